@@ -1,0 +1,92 @@
+/*
+ * xsknf_gpu.h -- C ABI of the MI355X checksummer batch path.
+ *
+ * The reference calls one user function per received frame,
+ *     int xsknf_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex);
+ * (reference src/xsknf.h:19-23), once per rx descriptor from the per-frame loop of
+ * process_batch_1if() (reference src/xsknf.c:654-672).  The checksummer's body is
+ * reference examples/checksummer/checksummer_user.c:30-112.
+ *
+ * This library replaces that per-frame loop with ONE call per rx batch: the
+ * whole batch of descriptors is handed over, every frame is checksummed on the
+ * GPU, the 2-byte UDP check field is rewritten in place in the UMEM and one
+ * verdict per frame is returned, with exactly the reference's meaning:
+ *     -1           drop  (frame goes back to the fill ring, src/xsknf.c:663-666)
+ *     0..n_if-1    transmit on that interface (tx ring, src/xsknf.c:667-671)
+ *
+ * Conventions (the reference's own): functions return 0 on success or a
+ * negative errno; no torch or HIP types appear in any signature (streams are
+ * passed as an opaque `void *` holding a hipStream_t; NULL = default stream).
+ */
+#ifndef XSKNF_GPU_H
+#define XSKNF_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same layout as struct xdp_desc (linux/if_xdp.h), i.e. exactly what the rx
+ * ring holds and what xsk_ring_cons__rx_desc() returns (src/xsknf.c:655-656). */
+struct xsknf_gpu_desc {
+	uint64_t addr;      /* UMEM address; unaligned mode: base | (offset << 48) */
+	uint32_t len;       /* frame length in bytes */
+	uint32_t options;
+};
+
+/* xsk_umem__add_offset_to_addr() (libxdp, used at src/xsknf.c:659) */
+#define XSKNF_GPU_UNALIGNED_BUF_OFFSET_SHIFT 48
+#define XSKNF_GPU_UNALIGNED_BUF_ADDR_MASK ((1ULL << XSKNF_GPU_UNALIGNED_BUF_OFFSET_SHIFT) - 1)
+
+/* enum action, examples/checksummer/checksummer_user.c:15-18 */
+#define XSKNF_CSUM_ACTION_REDIRECT 0
+#define XSKNF_CSUM_ACTION_DROP 1
+
+/* The three globals the reference callback reads (checksummer_user.c:24-25,28). */
+struct xsknf_csum_opts {
+	int32_t csum_iterations;   /* opt_csum_iterations (-i N), default 1; <= 0: no payload sum */
+	int32_t action;            /* opt_action (-c REDIRECT|DROP), default REDIRECT */
+	uint32_t num_interfaces;   /* config.num_interfaces (must be >= 1 for REDIRECT) */
+	uint32_t reserved;         /* must be 0 */
+};
+
+/* Library version: (major << 16) | minor. */
+uint32_t xsknf_gpu_version(void);
+
+/* Number of visible HIP devices in *count. */
+int xsknf_gpu_device_count(int *count);
+
+/*
+ * Checksum one rx batch, asynchronously on `stream`, on the current HIP device.
+ * Replaces the loop `for i in batch: verdict[i] = xsknf_packet_processor(pkt_i,
+ * len_i, ingress)` of src/xsknf.c:654-672 (pkt_i = umem + translated addr_i).
+ *
+ *   umem, umem_size   device-resident UMEM (hipMalloc'd, or a device mirror)
+ *   descs, n          device-resident rx descriptors (n may be 0)
+ *   ingress_ifindex   interface index of the rx socket (0 on the 1-iface path)
+ *   opts              host pointer, read before return
+ *   verdicts          device array of n int32, written by the kernel
+ *   frame_len_hint    largest frame length expected in the batch (0 = 2048);
+ *                     a performance hint only: every length is handled correctly
+ *   stream            hipStream_t or NULL
+ *
+ * Descriptors whose [addr, addr+len) lies outside [0, umem_size) are not
+ * touched and get verdict -1 (the kernel's own rx validation guarantees the
+ * reference never sees one).
+ * Returns 0, -EINVAL on bad arguments, -EIO on a HIP launch error.
+ */
+int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
+		const struct xsknf_gpu_desc *descs, uint32_t n,
+		uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+		int32_t *verdicts, uint32_t frame_len_hint, void *stream);
+
+/* Text of the last HIP error seen by this library on the calling thread. */
+const char *xsknf_gpu_last_error(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* XSKNF_GPU_H */

@@ -1,0 +1,74 @@
+"""The C-ABI library: builds for gfx950, loads without a GPU, and exports every
+function include/*.h declares.  Argument validation paths that return before
+any HIP call are exercised here too (no compute calls without a GPU)."""
+import ctypes
+import errno
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+from xsknf_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"\b(xsknf_gpu_\w+)\s*\(", src):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_header_declares_the_binding_list():
+    assert set(declared_functions()) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    for name in declared_functions():
+        assert re.search(rf"\bT {name}\b", out), f"{name} not exported as a text symbol"
+
+
+def test_library_has_gfx950_code_object():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}, targets
+
+
+def test_version():
+    assert _lib.load().xsknf_gpu_version() == 1
+
+
+def test_argument_validation_without_gpu():
+    lib = _lib.load()
+    f = lib.xsknf_gpu_checksum_batch
+    good = _lib.CsumOpts(1, _lib.ACTION_REDIRECT, 1, 0)
+    # n == 0 is a no-op
+    assert f(None, 0, None, 0, 0, ctypes.byref(good), None, 0, None) == 0
+    # NULL opts, bad action, REDIRECT with 0 interfaces, reserved != 0
+    assert f(None, 0, None, 0, 0, None, None, 0, None) == -errno.EINVAL
+    for bad in (_lib.CsumOpts(1, 2, 1, 0), _lib.CsumOpts(1, _lib.ACTION_REDIRECT, 0, 0),
+                _lib.CsumOpts(1, _lib.ACTION_DROP, 1, 7)):
+        assert f(None, 0, None, 5, 0, ctypes.byref(bad), None, 0, None) == -errno.EINVAL
+    # DROP does not need interfaces (the reference never divides in DROP mode)
+    assert f(None, 0, None, 0, 0, ctypes.byref(_lib.CsumOpts(1, _lib.ACTION_DROP, 0, 0)),
+             None, 0, None) == 0
+    # NULL buffers with n > 0
+    assert f(None, 0, None, 5, 0, ctypes.byref(good), None, 0, None) == -errno.EINVAL
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_lib.XsknfGpuError):
+        _lib.load()

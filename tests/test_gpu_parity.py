@@ -1,0 +1,164 @@
+"""Parity of the gfx950 batch path (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact -- every verdict and every UMEM byte (the kernel may change only
+the two UDP check bytes of frames that reach checksummer_user.c:108).
+Small seeded batches cover every branch of checksummer_user.c:30-112; the
+BASELINE configs run at full size (1M frames) against the threaded C oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle import csum_oracle as O
+from xsknf_amd import Checksummer, ChecksummerOptions, frames
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def run_gpu(b: frames.HostBatch, dev, *, ingress=0, iters=1, action=O.REDIRECT, nif=1, hint=0):
+    cs = Checksummer(ChecksummerOptions(action=action, csum_iterations=iters), num_interfaces=nif,
+                     frame_len_hint=hint)
+    umem = torch.from_numpy(b.umem).to(dev)
+    descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+    v = cs.process_batch(umem, descs, ingress_ifindex=ingress)
+    torch.cuda.synchronize()
+    return umem.cpu().numpy(), v.cpu().numpy()
+
+
+def run_oracle(b: frames.HostBatch, *, ingress=0, iters=1, action=O.REDIRECT, nif=1):
+    r = b.copy()
+    v = O.c_process_batch(r.umem, r.descs, ingress=ingress, iters=iters, action=action, nif=nif)
+    return r.umem, v
+
+
+def assert_parity(b, dev, **kw):
+    hint = kw.pop("hint", 0)
+    gu, gv = run_gpu(b, dev, hint=hint, **kw)
+    ou, ov = run_oracle(b, **kw)
+    bad = np.nonzero(gv != ov)[0]
+    assert bad.size == 0, f"verdict mismatch at {bad[:10]}: gpu {gv[bad[:10]]} oracle {ov[bad[:10]]}"
+    if not np.array_equal(gu, ou):
+        diff = np.nonzero(gu != ou)[0]
+        raise AssertionError(f"{diff.size} UMEM bytes differ, first at {diff[:10]}")
+    return gv
+
+
+def test_known_answers_through_gpu(dev):
+    from tests.test_oracle import KATS
+    for name, frame, kw, ret, sl, chk in KATS:
+        n = len(frame)
+        for rs in (0, 1, 5, 15):     # every 16-byte phase class incl. odd starts
+            umem = np.zeros(((rs + n + 255) // 256 + 1) * 256, dtype=np.uint8)
+            umem[256 + rs:256 + rs + n] = np.frombuffer(bytes(frame), dtype=np.uint8)
+            d = np.zeros(1, dtype=frames.DESC_DTYPE)
+            d["addr"], d["len"] = 256 + rs, n
+            b = frames.HostBatch(umem, d, "aligned")
+            gu, gv = run_gpu(b, dev, **kw)
+            assert gv[0] == ret, name
+            if chk is not None:
+                got = bytes(gu[256 + rs + sl[0]:256 + rs + sl[1]]).hex()
+                assert got == chk, f"{name} rs={rs}"
+
+
+@pytest.mark.parametrize("length", [60, 64, 65, 570, 1500, 1501, 4000, 9000, "imix"])
+@pytest.mark.parametrize("layout", ["aligned", "unaligned"])
+def test_seeded_batches_with_edge_cases(dev, length, layout):
+    n = 3000
+    if layout == "aligned":
+        chunk = 2048 if length == "imix" or length <= 1792 else 16384
+        b = frames.aligned_batch(n, length, chunk=chunk)
+    else:
+        b = frames.unaligned_batch(n, length)
+    frames.inject_edge_cases(b, 0.05)
+    assert_parity(b, dev, iters=1, action=O.REDIRECT, nif=1)
+
+
+@pytest.mark.parametrize("iters,action,nif,ingress", [
+    (1, O.DROP, 1, 0), (0, O.REDIRECT, 1, 0), (-3, O.REDIRECT, 2, 1), (2, O.REDIRECT, 3, 2),
+    (10, O.DROP, 1, 0), (50, O.REDIRECT, 4, 3), (7919, O.DROP, 1, 0)])
+def test_options(dev, iters, action, nif, ingress):
+    b = frames.unaligned_batch(2000, "imix", seed=iters & 0xFFFF)
+    frames.inject_edge_cases(b, 0.1)
+    assert_parity(b, dev, iters=iters, action=action, nif=nif, ingress=ingress)
+
+
+@pytest.mark.parametrize("hint", [1, 64, 100, 500, 1500, 4000, 9000, 60000])
+def test_frame_len_hint_is_only_a_hint(dev, hint):
+    """Every size class must handle every length (multi-pass loop, idle lanes)."""
+    rng = np.random.default_rng(hint)
+    lens = rng.integers(0, 12000, size=1500).astype(np.uint32)
+    b = frames.unaligned_batch(1500, lens, seed=hint)
+    frames.inject_edge_cases(b, 0.05)
+    assert_parity(b, dev, hint=hint, iters=3)
+
+
+def test_empty_and_tiny_batches(dev):
+    cs = Checksummer()
+    umem = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    descs = torch.zeros((0, 2), dtype=torch.int64, device=dev)
+    v = cs.process_batch(umem, descs)
+    assert v.numel() == 0
+    for n in (1, 2, 3, 17, 63, 64, 65, 257):
+        b = frames.aligned_batch(n, 64, chunk=2048, seed=n)
+        assert_parity(b, dev)
+
+
+def test_out_of_range_descriptors_are_dropped_untouched(dev):
+    b = frames.aligned_batch(64, 1500, chunk=2048)
+    size = b.umem.size
+    b.descs["addr"][3] = size - 10          # runs off the end
+    b.descs["addr"][7] = size + 4096        # starts past the end
+    b.descs["addr"][9] = (np.uint64(size - 100)) | (np.uint64(200) << np.uint64(48))
+    gu, gv = run_gpu(b, dev)
+    for i in (3, 7, 9):
+        assert gv[i] == -1
+    keep = np.ones(64, bool)
+    keep[[3, 7, 9]] = False
+    good = frames.HostBatch(b.umem.copy(), b.descs[keep].copy(), "aligned")
+    ou, ov = run_oracle(good)
+    assert np.array_equal(gv[keep], ov)
+    assert np.array_equal(gu, ou)
+
+
+def test_idempotent_reprocessing(dev):
+    """The check is cleared before summing, so a second pass changes nothing."""
+    b = frames.unaligned_batch(5000, "imix")
+    frames.inject_edge_cases(b, 0.05)
+    gu, gv = run_gpu(b, dev)
+    b2 = frames.HostBatch(gu.copy(), b.descs.copy(), b.layout)
+    gu2, gv2 = run_gpu(b2, dev)
+    assert np.array_equal(gu, gu2) and np.array_equal(gv, gv2)
+
+
+FULL = [
+    ("64B-aligned", 1 << 20, 64, "aligned"),
+    ("1500B-aligned", 1 << 20, 1500, "aligned"),
+    ("imix-aligned", 1 << 20, "imix", "aligned"),
+    ("9000B-unaligned", 1 << 20, 9000, "unaligned"),
+]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name,n,length,layout", FULL, ids=[f[0] for f in FULL])
+def test_full_size_configs_bit_exact(dev, name, n, length, layout):
+    """BASELINE configs 2-5 at full size, every byte compared with the oracle."""
+    umem, descs, lens = frames.device_batch(n, length, layout=layout, device=dev)
+    host_in = umem.cpu().numpy()
+    host_descs = descs.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1)
+    hint = int(lens.max())
+    v = Checksummer(frame_len_hint=hint).process_batch(umem, descs)
+    torch.cuda.synchronize()
+    _, ov = O.c_time_batch(host_in, host_descs, threads=16, reps=1)
+    gv = v.cpu().numpy()
+    assert np.array_equal(gv, ov)
+    assert np.array_equal(umem.cpu().numpy(), host_in)
+    # every synthetic frame is a valid UDP frame: all REDIRECT to iface 0
+    assert (gv == 0).all()

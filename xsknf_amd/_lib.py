@@ -1,0 +1,82 @@
+"""ctypes binding of the C ABI declared in include/xsknf_gpu.h.
+
+The product path is the gfx950 library ``xsknf_amd/lib/libxsknf_gpu.so`` built
+by ``make`` (or ``__graft_entry__.build()``).  There is no fallback: if the
+library is missing or fails to load, importing the binding raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libxsknf_gpu.so")
+
+# Every symbol include/xsknf_gpu.h declares (checked by tests/test_capi.py).
+EXPORTED_SYMBOLS = (
+    "xsknf_gpu_version",
+    "xsknf_gpu_device_count",
+    "xsknf_gpu_checksum_batch",
+    "xsknf_gpu_last_error",
+)
+
+ACTION_REDIRECT = 0
+ACTION_DROP = 1
+
+
+class CsumOpts(ctypes.Structure):
+    """struct xsknf_csum_opts (include/xsknf_gpu.h)."""
+
+    _fields_ = [
+        ("csum_iterations", ctypes.c_int32),
+        ("action", ctypes.c_int32),
+        ("num_interfaces", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+class XsknfGpuError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the gfx950 library once; raise loudly if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise XsknfGpuError(
+            f"{LIB_PATH} is missing: build it with `make` or __graft_entry__.build(); "
+            "there is no CPU fallback for the checksummer batch path")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.xsknf_gpu_version.restype = ctypes.c_uint32
+    lib.xsknf_gpu_version.argtypes = []
+    lib.xsknf_gpu_device_count.restype = ctypes.c_int
+    lib.xsknf_gpu_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    lib.xsknf_gpu_last_error.restype = ctypes.c_char_p
+    lib.xsknf_gpu_last_error.argtypes = []
+    lib.xsknf_gpu_checksum_batch.restype = ctypes.c_int
+    lib.xsknf_gpu_checksum_batch.argtypes = [
+        ctypes.c_void_p, ctypes.c_uint64,   # umem, umem_size
+        ctypes.c_void_p, ctypes.c_uint32,   # descs, n
+        ctypes.c_uint32,                    # ingress_ifindex
+        ctypes.POINTER(CsumOpts),           # opts
+        ctypes.c_void_p,                    # verdicts
+        ctypes.c_uint32,                    # frame_len_hint
+        ctypes.c_void_p,                    # stream
+    ]
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().xsknf_gpu_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise XsknfGpuError(f"{what} failed: rc={rc} ({os.strerror(-rc) if rc < 0 else rc}); "
+                            f"last HIP error: {last_error()!r}")

@@ -1,0 +1,243 @@
+"""Host-side mirror of the reference checksummer NF over the gfx950 batch path.
+
+Reference: examples/checksummer/checksummer_user.c
+  * enum action {REDIRECT, DROP}                        :15-18
+  * opt_action / opt_csum_iterations                    :24-25
+  * xsknf_packet_processor(pkt, len, ingress_ifindex)   :30-112 (per frame)
+  * parse_command_line(), getopt "qxai:c:"              :139-175
+and the library option parser src/xsknf.c:777-874 (xsknf_parse_args, getopt
+"i:pSf:ub:BM:w:"), whose frame size / unaligned / batch size decide the UMEM
+layout the batch path reads.
+
+The per-frame callback becomes `Checksummer.process_batch()`: one call per rx
+batch, device-resident UMEM + descriptors, verdicts with the callback's meaning
+(-1 drop, else tx interface).  Everything runs in libxsknf_gpu.so; there is no
+CPU fallback (a missing library raises at construction).
+"""
+from __future__ import annotations
+
+import ctypes
+import getopt
+import sys
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from . import _lib
+
+ACTION_REDIRECT = _lib.ACTION_REDIRECT
+ACTION_DROP = _lib.ACTION_DROP
+XSKNF_MAX_INTERFACES = 32          # src/xsknf.h:11
+XSKNF_MAX_WORKERS = 32             # src/xsknf.h:12
+MODE_AF_XDP = 0x1                  # src/xsknf.h:15-17
+MODE_XDP = 0x2
+MODE_COMBINED = MODE_AF_XDP | MODE_XDP
+XSK_UMEM_DEFAULT_FRAME_SIZE = 4096  # libxdp default (src/xsknf.c:48)
+
+_APP_USAGE = (
+    "  Usage: %s [XSKNF_OPTIONS] -- [APP_OPTIONS]\n"
+    "  App options:\n"
+    "  -c, --action\t\tREDIRECT or DROP packets (default REDIRECT).\n"
+    "  -i, --csum-iterations\tNumber of times to recompute the checksum.\n"
+    "  -q, --quiet\t\tDo not display any stats.\n"
+    "  -x, --extra-stats\tDisplay extra statistics.\n"
+    "  -a, --app-stats\tDisplay application (syscall) statistics.\n"
+    "\n")
+
+
+def _usage_exit(prog: str) -> None:
+    sys.stderr.write(_APP_USAGE % prog)
+    sys.exit(1)   # EXIT_FAILURE, as usage() does at checksummer_user.c:136
+
+
+@dataclass
+class ChecksummerOptions:
+    """The checksummer app globals (checksummer_user.c:20-25)."""
+    action: int = ACTION_REDIRECT
+    csum_iterations: int = 1
+    quiet: bool = False
+    extra_stats: bool = False
+    app_stats: bool = False
+
+
+def _atoi(s: str) -> int:
+    """C atoi(): leading whitespace, optional sign, digits; 0 if none."""
+    s = s.lstrip()
+    i, sign = 0, 1
+    if i < len(s) and s[i] in "+-":
+        sign = -1 if s[i] == "-" else 1
+        i += 1
+    j = i
+    while j < len(s) and s[j].isdigit():
+        j += 1
+    v = int(s[i:j]) if j > i else 0
+    v *= sign
+    return ((v + 2**31) % 2**32) - 2**31
+
+
+def parse_command_line(argv: List[str], prog: str = "checksummer") -> ChecksummerOptions:
+    """Mirror of parse_command_line() (checksummer_user.c:139-175).
+
+    `argv` are the APP options (after `--`).  An invalid action prints
+    "ERROR: invalid action X" plus usage and exits with status 1, like the
+    reference.  The reference declares --csum-iterations as no_argument
+    (:116) so only `-i N` works there; here the long form requires an argument
+    rather than crashing on atoi(NULL)."""
+    o = ChecksummerOptions()
+    try:
+        opts, _ = getopt.getopt(argv, "qxai:c:",
+                                ["action=", "csum-iterations=", "quiet", "extra-stats", "app-stats"])
+    except getopt.GetoptError:
+        _usage_exit(prog)
+    for k, v in opts:
+        if k in ("-c", "--action"):
+            if v == "REDIRECT":
+                o.action = ACTION_REDIRECT
+            elif v == "DROP":
+                o.action = ACTION_DROP
+            else:
+                sys.stderr.write(f"ERROR: invalid action {v}\n")
+                _usage_exit(prog)
+        elif k in ("-i", "--csum-iterations"):
+            o.csum_iterations = _atoi(v)
+        elif k in ("-q", "--quiet"):
+            o.quiet = True
+        elif k in ("-x", "--extra-stats"):
+            o.extra_stats = True
+        elif k in ("-a", "--app-stats"):
+            o.app_stats = True
+    return o
+
+
+@dataclass
+class XsknfConfig:
+    """struct xsknf_config (src/xsknf.h:25-40) with the defaults of src/xsknf.c:46-52."""
+    interfaces: List[str] = field(default_factory=list)
+    bind_flags: List[str] = field(default_factory=list)   # "", "copy" or "zerocopy"
+    workers: int = 1
+    working_mode: int = MODE_AF_XDP
+    skb_mode: bool = False
+    batch_size: int = 64
+    poll: bool = False
+    unaligned_chunks: bool = False
+    xsk_frame_size: int = XSK_UMEM_DEFAULT_FRAME_SIZE
+    busy_poll: bool = False
+
+    @property
+    def num_interfaces(self) -> int:
+        return len(self.interfaces)
+
+
+def parse_args(argv: List[str]) -> tuple:
+    """Mirror of xsknf_parse_args (src/xsknf.c:777-874): returns (config, app_argv).
+
+    Errors follow the reference: unknown copy mode / mode / workers < 1 / no
+    interface / non-power-of-two frame size in aligned mode -> message + exit(1)."""
+    cfg = XsknfConfig()
+    if "--" in argv:
+        cut = argv.index("--")
+        lib_argv, app_argv = argv[:cut], argv[cut + 1:]
+    else:
+        lib_argv, app_argv = argv, []
+    try:
+        opts, _ = getopt.getopt(lib_argv, "i:pSf:ub:BM:w:",
+                                ["iface=", "poll", "xdp-skb", "frame-size=", "unaligned",
+                                 "batch-size=", "busy-poll", "mode=", "workers="])
+    except getopt.GetoptError as e:
+        sys.stderr.write(f"ERROR: {e}\n")
+        sys.exit(1)
+    for k, v in opts:
+        if k in ("-i", "--iface"):
+            name, _, mode = v.partition(":")
+            if mode and mode not in ("c", "z"):
+                sys.stderr.write(f"ERROR: unknown copy mode '{mode[0]}'\n")
+                sys.exit(1)
+            cfg.interfaces.append(name)
+            cfg.bind_flags.append({"": "", "c": "copy", "z": "zerocopy"}[mode[:1]])
+        elif k in ("-p", "--poll"):
+            cfg.poll = True
+        elif k in ("-S", "--xdp-skb"):
+            cfg.skb_mode = True
+        elif k in ("-u", "--unaligned"):
+            cfg.unaligned_chunks = True
+        elif k in ("-f", "--frame-size"):
+            cfg.xsk_frame_size = _atoi(v)
+        elif k in ("-b", "--batch-size"):
+            cfg.batch_size = _atoi(v)
+        elif k in ("-B", "--busy-poll"):
+            cfg.busy_poll = True
+        elif k in ("-M", "--mode"):
+            m = {"AF_XDP": MODE_AF_XDP, "XDP": MODE_XDP, "COMBINED": MODE_COMBINED}.get(v)
+            if m is None:
+                sys.stderr.write(f"ERROR: unknown working mode {v}\n")
+                sys.exit(1)
+            cfg.working_mode = m
+        elif k in ("-w", "--workers"):
+            cfg.workers = _atoi(v)
+            if cfg.workers < 1:
+                sys.stderr.write(f"ERROR: Invalid number of workers {cfg.workers}")
+                sys.exit(1)
+    if not cfg.interfaces:
+        sys.stderr.write("ERROR: at least one interface in required\n")
+        sys.exit(1)
+    fs = cfg.xsk_frame_size
+    if (fs & (fs - 1)) and not cfg.unaligned_chunks:
+        sys.stderr.write(f"--frame-size={fs} is not a power of two\n")
+        sys.exit(1)
+    return cfg, app_argv
+
+
+class Checksummer:
+    """The checksummer NF bound to the gfx950 batch kernel.
+
+    `process_batch` replaces the per-frame loop of process_batch_1if
+    (src/xsknf.c:654-672): for every descriptor it performs exactly
+    xsknf_packet_processor(umem + addr, len, ingress) -- the UDP check is
+    rewritten in place in `umem` and the verdict stored in `verdicts`."""
+
+    def __init__(self, options: Optional[ChecksummerOptions] = None, num_interfaces: int = 1,
+                 frame_len_hint: int = 0):
+        self.options = options or ChecksummerOptions()
+        self.num_interfaces = int(num_interfaces)
+        self.frame_len_hint = int(frame_len_hint)
+        self._lib = _lib.load()
+
+    def csum_opts(self) -> _lib.CsumOpts:
+        return _lib.CsumOpts(int(self.options.csum_iterations), int(self.options.action),
+                             self.num_interfaces, 0)
+
+    def process_batch_ptr(self, umem_ptr: int, umem_size: int, descs_ptr: int, n: int,
+                          verdicts_ptr: int, ingress_ifindex: int = 0, stream: int = 0,
+                          frame_len_hint: Optional[int] = None) -> None:
+        """Raw-pointer form (device pointers), asynchronous on `stream`."""
+        hint = self.frame_len_hint if frame_len_hint is None else int(frame_len_hint)
+        opts = self.csum_opts()
+        rc = self._lib.xsknf_gpu_checksum_batch(
+            ctypes.c_void_p(umem_ptr), umem_size, ctypes.c_void_p(descs_ptr), n,
+            ingress_ifindex, ctypes.byref(opts), ctypes.c_void_p(verdicts_ptr), hint,
+            ctypes.c_void_p(stream or None))
+        _lib.check(rc, "xsknf_gpu_checksum_batch")
+
+    def process_batch(self, umem, descs, ingress_ifindex: int = 0, verdicts=None,
+                      frame_len_hint: Optional[int] = None, stream=None):
+        """Torch-tensor form: `umem` uint8 and `descs` (n,2) int64 / (n,16) uint8
+        tensors on the same GPU.  Returns the int32 verdict tensor."""
+        import torch
+
+        if not umem.is_cuda or not descs.is_cuda:
+            raise ValueError("umem and descs must be device tensors (no CPU path)")
+        if umem.dtype != torch.uint8 or not umem.is_contiguous():
+            raise ValueError("umem must be a contiguous uint8 tensor")
+        if not descs.is_contiguous() or descs.numel() * descs.element_size() % 16:
+            raise ValueError("descs must be a contiguous array of 16-byte xdp_desc")
+        n = descs.numel() * descs.element_size() // 16
+        if verdicts is None:
+            verdicts = torch.empty(n, dtype=torch.int32, device=umem.device)
+        elif verdicts.dtype != torch.int32 or verdicts.numel() < n or not verdicts.is_contiguous():
+            raise ValueError("verdicts must be a contiguous int32 tensor with >= n entries")
+        if stream is None:
+            stream = torch.cuda.current_stream(umem.device)
+        with torch.cuda.device(umem.device):
+            self.process_batch_ptr(umem.data_ptr(), umem.numel(), descs.data_ptr(), n,
+                                   verdicts.data_ptr(), ingress_ifindex, stream.cuda_stream,
+                                   frame_len_hint)
+        return verdicts
