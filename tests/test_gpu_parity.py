@@ -128,14 +128,20 @@ def test_out_of_range_descriptors_are_dropped_untouched(dev):
     assert np.array_equal(gu, ou)
 
 
-def test_idempotent_reprocessing(dev):
-    """The check is cleared before summing, so a second pass changes nothing."""
+def test_reprocessing(dev):
+    """A second pass over processed frames matches the oracle run on them, and on
+    well-formed frames (ihl 5) it changes nothing: the check is cleared before
+    summing.  (With ihl 2 or 3 the UDP check overlaps the IP addresses the
+    pseudo-header reads, so there the second pass legitimately differs.)"""
     b = frames.unaligned_batch(5000, "imix")
     frames.inject_edge_cases(b, 0.05)
     gu, gv = run_gpu(b, dev)
     b2 = frames.HostBatch(gu.copy(), b.descs.copy(), b.layout)
-    gu2, gv2 = run_gpu(b2, dev)
-    assert np.array_equal(gu, gu2) and np.array_equal(gv, gv2)
+    assert_parity(b2, dev)
+    clean = frames.unaligned_batch(5000, "imix", seed=99)
+    cu, cv = run_gpu(clean, dev)
+    cu2, cv2 = run_gpu(frames.HostBatch(cu.copy(), clean.descs.copy(), clean.layout), dev)
+    assert np.array_equal(cu, cu2) and np.array_equal(cv, cv2)
 
 
 FULL = [
