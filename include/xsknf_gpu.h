@@ -82,6 +82,30 @@ int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
 		uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
 		int32_t *verdicts, uint32_t frame_len_hint, void *stream);
 
+/*
+ * Launch shape of the batch kernel (tuning / benchmarking).  A group of
+ * `lanes_per_frame` lanes (8, 16, 32 or 64) owns one frame at a time and loads
+ * `chunks_per_lane` 16-byte chunks per pass; `frames_per_group` frames have
+ * their loads in flight together; the persistent grid has `blocks_per_cu`
+ * 256-thread blocks per CU (0 = 8).  Only instantiated shapes are accepted
+ * (-EINVAL otherwise); every shape gives identical results.
+ */
+struct xsknf_gpu_launch_cfg {
+	int32_t lanes_per_frame;
+	int32_t chunks_per_lane;
+	int32_t frames_per_group;
+	int32_t blocks_per_cu;
+};
+
+/* The shape xsknf_gpu_checksum_batch() uses for a given frame_len_hint. */
+int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg);
+
+/* xsknf_gpu_checksum_batch() with an explicit launch shape instead of a hint. */
+int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size,
+		const struct xsknf_gpu_desc *descs, uint32_t n,
+		uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+		int32_t *verdicts, const struct xsknf_gpu_launch_cfg *cfg, void *stream);
+
 /* Text of the last HIP error seen by this library on the calling thread. */
 const char *xsknf_gpu_last_error(void);
 

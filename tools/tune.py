@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""A/B the launch shapes of the checksummer kernel in ONE process (interleaved
+rounds, median of per-round HIP-event timings), on device-resident batches.
+
+    python tools/tune.py --workload 1500 --variants 32,3,2:32,3,1:64,2,1 [--bpc 8,4]
+
+Every variant's output (verdicts + whole UMEM) is compared with the default
+shape's output, so a tuning run is also a cross-variant parity check.
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+from xsknf_amd import _lib, frames  # noqa: E402
+
+WL = {
+    "1500": (1500, "aligned"), "64": (64, "aligned"), "imix": ("imix", "aligned"),
+    "jumbo": (9000, "unaligned"), "570": (570, "aligned"),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="1500")
+    ap.add_argument("--variants", default="")
+    ap.add_argument("--bpc", default="8")
+    ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    length, layout = WL[a.workload]
+    dev = torch.device("cuda:0")
+    umem0, descs, lens = frames.device_batch(a.frames, length, layout=layout, device=dev)
+    lib = _lib.load()
+    opts = _lib.CsumOpts(1, 0, 1, 0)
+    n = a.frames
+    hint = int(lens.max())
+    dflt = _lib.LaunchCfg()
+    lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(dflt))
+    shapes = [(dflt.lanes_per_frame, dflt.chunks_per_lane, dflt.frames_per_group)]
+    for t in [x for x in a.variants.split(":") if x]:
+        s = tuple(int(y) for y in t.split(","))
+        if s not in shapes:
+            shapes.append(s)
+    bpcs = [int(x) for x in a.bpc.split(",")]
+    cfgs = [(s, b) for s in shapes for b in bpcs]
+    stream = torch.cuda.current_stream()
+    umem = umem0.clone()
+    verd = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def run(cfg, um, vv):
+        c = _lib.LaunchCfg(cfg[0][0], cfg[0][1], cfg[0][2], cfg[1])
+        rc = lib.xsknf_gpu_checksum_batch_cfg(ctypes.c_void_p(um.data_ptr()), um.numel(),
+                                              ctypes.c_void_p(descs.data_ptr()), n, 0,
+                                              ctypes.byref(opts), ctypes.c_void_p(vv.data_ptr()),
+                                              ctypes.byref(c), ctypes.c_void_p(stream.cuda_stream))
+        _lib.check(rc, f"cfg {cfg}")
+
+    # reference output = default shape on a fresh copy
+    ref_u = umem0.clone()
+    ref_v = torch.empty_like(verd)
+    run(cfgs[0], ref_u, ref_v)
+    torch.cuda.synchronize()
+    times = {c: [] for c in cfgs}
+    ok = {}
+    for c in cfgs:
+        u = umem0.clone()
+        v = torch.empty_like(verd)
+        run(c, u, v)
+        torch.cuda.synchronize()
+        ok[c] = bool(torch.equal(u, ref_u) and torch.equal(v, ref_v))
+        del u, v
+    for r in range(a.rounds):
+        for c in cfgs:
+            for _ in range(2):
+                run(c, umem, verd)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(a.reps):
+                run(c, umem, verd)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[c].append(e0.elapsed_time(e1) / a.reps * 1e3)
+    blen = int(lens.sum())
+    alg = blen + n * 22
+    for c in cfgs:
+        med = statistics.median(times[c])
+        print(json.dumps({"workload": a.workload, "shape": c[0], "bpc": c[1], "us": round(med, 2),
+                          "min_us": round(min(times[c]), 2),
+                          "gbs_checksummed": round(blen / med / 1e3, 1),
+                          "roofline_frac": round(alg / med / 1e3 / 8000, 4),
+                          "mpps": round(n / med, 1), "matches_default": ok[c]}))
+
+
+if __name__ == "__main__":
+    main()

@@ -18,6 +18,8 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_device_count",
     "xsknf_gpu_checksum_batch",
     "xsknf_gpu_last_error",
+    "xsknf_gpu_default_launch_cfg",
+    "xsknf_gpu_checksum_batch_cfg",
 )
 
 ACTION_REDIRECT = 0
@@ -32,6 +34,17 @@ class CsumOpts(ctypes.Structure):
         ("action", ctypes.c_int32),
         ("num_interfaces", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
+    ]
+
+
+class LaunchCfg(ctypes.Structure):
+    """struct xsknf_gpu_launch_cfg (include/xsknf_gpu.h)."""
+
+    _fields_ = [
+        ("lanes_per_frame", ctypes.c_int32),
+        ("chunks_per_lane", ctypes.c_int32),
+        ("frames_per_group", ctypes.c_int32),
+        ("blocks_per_cu", ctypes.c_int32),
     ]
 
 
@@ -67,6 +80,13 @@ def load() -> ctypes.CDLL:
         ctypes.c_void_p,                    # verdicts
         ctypes.c_uint32,                    # frame_len_hint
         ctypes.c_void_p,                    # stream
+    ]
+    lib.xsknf_gpu_default_launch_cfg.restype = ctypes.c_int
+    lib.xsknf_gpu_default_launch_cfg.argtypes = [ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]
+    lib.xsknf_gpu_checksum_batch_cfg.restype = ctypes.c_int
+    lib.xsknf_gpu_checksum_batch_cfg.argtypes = [
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+        ctypes.POINTER(CsumOpts), ctypes.c_void_p, ctypes.POINTER(LaunchCfg), ctypes.c_void_p,
     ]
     _lib = lib
     return lib

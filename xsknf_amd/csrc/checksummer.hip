@@ -38,7 +38,8 @@ namespace xsknf_gpu {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kHdrChunks = 7;   // (15 + 74 + 8 + 15) / 16 rounded up: max rel offset of f[u+7] is 15+81
+constexpr int kHdrChunks = 7;   // window chunks 0..6 hold frame bytes [0, 97) at any 16-byte phase
+constexpr int kSlotBytes = 128; // per-frame LDS slot: 16 B lead-in (shift by -rs) + 7 chunks
 
 __device__ __forceinline__ uint64_t umem_offset(uint64_t addr) {
   return (addr & XSKNF_GPU_UNALIGNED_BUF_ADDR_MASK) + (addr >> XSKNF_GPU_UNALIGNED_BUF_OFFSET_SHIFT);
@@ -77,6 +78,9 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v) {
   return v;
 }
 
+// write-only sink for the unconditional stores of frames that write nothing
+__device__ uint32_t g_sink[4];
+
 struct KernelArgs {
   uint8_t *umem;
   uint64_t umem_size;
@@ -85,121 +89,239 @@ struct KernelArgs {
   uint32_t n;
   uint32_t payload_mult;   // max(csum_iterations, 0)
   int32_t fwd_verdict;     // REDIRECT ? (ingress+1) % n_if : -1
+  const uint4 *dummy;      // readable 16-byte block for frames that need no bytes
 };
 
+// Where a frame's bytes are and which 16-byte chunks cover them.  Frames that
+// need no bytes (len < 14, or a descriptor outside the UMEM) point at a dummy
+// 16-byte block so that every chunk load of the pipeline can be unconditional.
+struct FrameRef {
+  const uint4 *cp;   // 16-byte aligned window start (cp <= fp)
+  uint8_t *fp;       // first byte of the frame
+  int rs;            // fp - cp, 0..15
+  int len;
+  int nch;           // chunks in the window, >= 1
+  bool exists;       // index < n
+  bool live;         // exists, in range and len >= 14
+};
+
+__device__ __forceinline__ FrameRef make_ref(const KernelArgs &a, const xsknf_gpu_desc &d, bool exists) {
+  FrameRef r;
+  const uint64_t off = umem_offset(d.addr);
+  const uint32_t len = d.len;
+  const bool in_range = off <= a.umem_size && len <= a.umem_size - off;
+  r.exists = exists;
+  r.live = exists && in_range && len >= 14;
+  r.len = static_cast<int>(len);
+  if (r.live) {
+    r.fp = a.umem + off;
+    r.rs = static_cast<int>(reinterpret_cast<uintptr_t>(r.fp) & 15);
+    r.cp = reinterpret_cast<const uint4 *>(r.fp - r.rs);
+    r.nch = (r.rs + r.len + 15) >> 4;
+  } else {
+    r.fp = a.umem;
+    r.rs = 0;
+    r.cp = a.dummy;
+    r.nch = 1;
+  }
+  return r;
+}
+
+// Issue this lane's NCH chunk loads of pass `p0` (chunk index clamped into the
+// window: lanes past the end re-read the last chunk, which costs no HBM bytes
+// and keeps the loads free of branches so the next frame's loads stay in
+// flight while the current frame is reduced).
 template <int LPF, int NCH>
+__device__ __forceinline__ void load_pass(const FrameRef &r, int p0, int gl, uint4 (&v)[NCH]) {
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = min(p0 + k * LPF + gl, r.nch - 1);
+    v[k] = r.cp[c];
+  }
+}
+
+// The two stores a frame produces (check bytes, verdict).  They are issued at
+// the start of the NEXT step, before that step's loads, and by every lane
+// unconditionally (lanes of a group write identical values to one address;
+// frames with nothing to write aim at a sink word).  No store then sits
+// between a frame's loads and their use, nor inside a branch, so the compiler
+// can wait for exactly the loads it needs instead of draining vmcnt.
+struct PendingStores {
+  uint16_t *cdst;
+  int32_t *vdst;
+  uint32_t check;
+  int32_t verdict;
+};
+
+__device__ __forceinline__ PendingStores sink_stores() {
+  return PendingStores{reinterpret_cast<uint16_t *>(g_sink), reinterpret_cast<int32_t *>(g_sink + 1), 0u, 0};
+}
+
+__device__ __forceinline__ void issue(const PendingStores &ps) {
+  *ps.cdst = static_cast<uint16_t>(ps.check);      // :108
+  *ps.vdst = ps.verdict;
+}
+
+template <int LPF, int NCH>
+__device__ __forceinline__ PendingStores process_frame(const KernelArgs &args, const FrameRef &r,
+                                                       uint32_t f, const uint4 (&v)[NCH],
+                                                       uint8_t *slot, int gl) {
+  constexpr int SPAN = LPF * NCH;
+  // Stage window chunks 0..6 in LDS shifted by -rs, so frame byte i sits at
+  // slot[16 + i] whatever the frame's alignment: the header fields are then at
+  // fixed offsets.  One wave's LDS accesses execute in issue order; only the
+  // compiler must be kept from moving the reads above the writes.
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = k * LPF + gl;
+    if (k * LPF < kHdrChunks && c < kHdrChunks)
+      *reinterpret_cast<uint4 *>(slot + 16 + 16 * c - r.rs) = v[k];
+  }
+  compiler_barrier();
+  const uint4 q0 = *reinterpret_cast<const uint4 *>(slot + 16);   // f[0..15]
+  const uint4 q1 = *reinterpret_cast<const uint4 *>(slot + 32);   // f[16..31]
+  const uint32_t w8 = *reinterpret_cast<const uint32_t *>(slot + 48);  // f[32..35]
+  const int ihl = (q0.w >> 16) & 0x0f;                             // f[14] low nibble
+  const int u = 14 + 4 * ihl;                                      // :52, ihl unvalidated
+  const uint32_t wa = *reinterpret_cast<const uint32_t *>(slot + 16 + u + 2);  // f[u+2..u+5]
+  const uint32_t wb = *reinterpret_cast<const uint32_t *>(slot + 16 + u + 6);  // f[u+6..u+9]
+  compiler_barrier();
+
+  const bool ipv4 = (q0.w & 0xffffu) == 0x0008u;                  // f[12..13] == 08 00
+  const bool udp = (q1.y >> 24) == 17u;                           // f[23]
+  int32_t verdict;
+  bool do_sum = false;
+  if (!r.live) {
+    verdict = -1;                                   // :34-37 (and out-of-range descriptors)
+  } else if (!ipv4) {
+    verdict = 0;                                    // :39-41
+  } else if (r.len < 34) {
+    verdict = -1;                                   // :43-46
+  } else if (!udp) {
+    verdict = 0;                                    // :48-50
+  } else if (u + 8 > r.len) {
+    verdict = -1;                                   // :53-55
+  } else {
+    verdict = args.fwd_verdict;                     // :110-111
+    do_sum = true;
+  }
+
+  // Pass-0 partial sums on every path (also for frames that end up unsummed):
+  // every loaded register is consumed unconditionally, so no load of this frame
+  // can still be in flight at the loop back-edge.
+  const int lo = r.rs + u;
+  const int hi = r.rs + r.len;
+  const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+  const uint32_t wh = wl << 8 | wl >> 24;
+  uint32_t acc_lo = 0, acc_hi = 0;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+
+  uint16_t check = 0;
+  if (do_sum) {
+    // :57-65 pseudo-header, read before the check is cleared:
+    // le16(26) + le16(28) + le16(30) + le16(32) + 17<<8 + le16(u+4)
+    uint32_t s = (q1.z >> 16) + (q1.w & 0xffffu) + (q1.w >> 16) + (w8 & 0xffffu) + 0x1100u + (wa >> 16);
+    const uint32_t old_check = wb & 0xffffu;        // counted as 0 (:68)
+    for (int p = SPAN; p < r.nch; p += SPAN) {      // frames longer than one pass
+      uint4 t[NCH];
+      load_pass<LPF, NCH>(r, p, gl, t);
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) chunk_sum(t[k], (p + k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+    }
+    uint32_t P = group_sum<LPF>(acc_lo + (acc_hi << 8));
+    P -= old_check;
+    s += args.payload_mult * P;                     // :92-103, iterations in closed form
+    check = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));  // :105-106
+  }
+  PendingStores ps;
+  ps.cdst = do_sum ? reinterpret_cast<uint16_t *>(r.fp + u + 6) : reinterpret_cast<uint16_t *>(g_sink);
+  ps.vdst = r.exists ? args.verdicts + f : reinterpret_cast<int32_t *>(g_sink + 1);
+  ps.check = check;
+  ps.verdict = verdict;
+  compiler_barrier();   // the next frame rewrites this group's LDS slot
+  return ps;
+}
+
+// The G descriptors of one wave's frames are contiguous, so they are fetched
+// with wave-uniform scalar loads (s_load, counted by lgkmcnt): the descriptor
+// prefetch then never forces the compiler to drain the vector-memory counter
+// that the chunk loads of the next frame are still running on.
+typedef const __attribute__((address_space(4))) xsknf_gpu_desc *const_desc_ptr;
+
+template <int G>
+struct DescSet {
+  uint64_t addr[G];
+  uint32_t len[G];
+};
+
+template <int G>
+__device__ __forceinline__ DescSet<G> load_descs(const KernelArgs &a, uint32_t wf, uint32_t last) {
+  DescSet<G> ds;
+  const const_desc_ptr cd = (const_desc_ptr)(reinterpret_cast<uintptr_t>(a.descs));
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint32_t i = min(wf + g, last);
+    ds.addr[g] = cd[i].addr;
+    ds.len[g] = cd[i].len;
+  }
+  return ds;
+}
+
+template <int G>
+__device__ __forceinline__ xsknf_gpu_desc pick(const DescSet<G> &ds, int grp) {
+  xsknf_gpu_desc d;
+  d.addr = ds.addr[0];
+  d.len = ds.len[0];
+#pragma unroll
+  for (int g = 1; g < G; ++g) {
+    d.addr = grp == g ? ds.addr[g] : d.addr;
+    d.len = grp == g ? ds.len[g] : d.len;
+  }
+  d.options = 0;
+  return d;
+}
+
+template <int LPF, int NCH, int U>
 __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args) {
   static_assert(kWave % LPF == 0, "LPF must divide the wave");
   static_assert(LPF * NCH >= kHdrChunks, "pass 0 must cover the header window");
-  constexpr int G = kWave / LPF;     // frames in flight per wave
-  constexpr int SPAN = LPF * NCH;    // chunks per pass
+  constexpr int G = kWave / LPF;     // frame groups per wave
+  constexpr int FW = G * U;          // frames per wave per iteration
+  static_assert(FW <= 8, "descriptor prefetch is held in SGPRs");
 
-  __shared__ uint4 hdr[kWavesPerBlock][G][kHdrChunks];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock][G][kSlotBytes];
 
   const int lane = threadIdx.x & (kWave - 1);
-  const int wv = threadIdx.x / kWave;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int grp = lane / LPF;
   const int gl = lane % LPF;
-  const uint32_t stride = gridDim.x * kWavesPerBlock * G;
-  uint32_t f = (blockIdx.x * kWavesPerBlock + wv) * G + grp;
+  uint8_t *slot = &lds[wv][grp][0];
+  const uint32_t wstride = gridDim.x * kWavesPerBlock * FW;   // frames per grid sweep
+  const uint32_t last = args.n - 1;
+  uint32_t wf = (blockIdx.x * kWavesPerBlock + wv) * FW;      // this wave's first frame
 
-  xsknf_gpu_desc d;
-  if (f < args.n) d = args.descs[f];
-
-  for (; f < args.n; f += stride) {
-    const uint64_t off = umem_offset(d.addr);
-    const uint32_t len = d.len;
-    // prefetch the next descriptor of this group while this frame is worked on
-    const uint32_t fn = f + stride;
-    xsknf_gpu_desc dn;
-    if (fn < args.n) dn = args.descs[fn];
-
-    if (off > args.umem_size || len > args.umem_size - off) {
-      if (gl == 0) args.verdicts[f] = -1;
-      d = dn;
-      continue;
-    }
-
-    uint8_t *fp = args.umem + off;
-    // 16-byte aligned window around the frame, kept as an offset from the kernel
-    // argument so the compiler keeps global (not flat) addressing
-    const int rs = static_cast<int>(reinterpret_cast<uintptr_t>(fp) & 15);
-    const uint4 *cp = reinterpret_cast<const uint4 *>(fp - rs);
-    const int nch = (rs + static_cast<int>(len) + 15) >> 4;
-
-    uint4 v[NCH];
+  // Each iteration issues the chunk loads of U frames per group at once, then
+  // reduces them one by one (frame u+1's loads stay in flight while frame u is
+  // parsed and summed).  Nothing is carried in flight across the back-edge:
+  // descriptors for the next iteration are prefetched with scalar loads.
+  DescSet<FW> dcur = load_descs<FW>(args, wf, last);
+  while (wf < args.n) {          // wave-uniform loop control
+    FrameRef ref[U];
+    uint4 v[U][NCH];
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int c = k * LPF + gl;
-      v[k] = (c < nch) ? cp[c] : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < U; ++u) {
+      const uint32_t f = wf + u * G + grp;
+      ref[u] = make_ref(args, pick<FW>(dcur, u * G + grp), f < args.n);
+      load_pass<LPF, NCH>(ref[u], 0, gl, v[u]);
     }
-
-    // stage the header window; one wave's LDS accesses execute in issue order,
-    // so only the compiler has to be kept from moving the reads above the writes
+    const uint32_t wn = wf + wstride;
+    dcur = load_descs<FW>(args, wn, last);
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int c = k * LPF + gl;
-      if (k * LPF < kHdrChunks && c < kHdrChunks && c < nch) hdr[wv][grp][c] = v[k];
+    for (int u = 0; u < U; ++u) {
+      issue(process_frame<LPF, NCH>(args, ref[u], wf + u * G + grp, v[u], slot, gl));
     }
-    compiler_barrier();
-    const uint8_t *h = reinterpret_cast<const uint8_t *>(&hdr[wv][grp][0]) + rs;
-
-    int32_t verdict;
-    int u = 0;
-    bool do_sum = false;
-    if (len < 14) {
-      verdict = -1;                                   // :34-37
-    } else if (h[12] != 0x08 || h[13] != 0x00) {
-      verdict = 0;                                    // :39-41
-    } else if (len < 34) {
-      verdict = -1;                                   // :43-46
-    } else if (h[23] != 17) {
-      verdict = 0;                                    // :48-50
-    } else {
-      u = 14 + ((h[14] & 0x0f) << 2);                 // :52, ihl unvalidated
-      if (u + 8 > static_cast<int>(len)) {
-        verdict = -1;                                 // :53-55
-      } else {
-        verdict = args.fwd_verdict;                   // :110-111
-        do_sum = true;
-      }
-    }
-
-    if (do_sum) {
-      auto le16 = [&](int i) -> uint32_t { return h[i] | (static_cast<uint32_t>(h[i + 1]) << 8); };
-      // :57-65 pseudo-header (read before the check is cleared)
-      uint32_t s = le16(26) + le16(28) + le16(30) + le16(32) + 0x1100u + le16(u + 4);
-      const uint32_t old_check = le16(u + 6);         // counted as 0 (:68)
-
-      const int lo = rs + u;
-      const int hi = rs + static_cast<int>(len);
-      const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
-      const uint32_t wh = wl << 8 | wl >> 24;
-      uint32_t acc_lo = 0, acc_hi = 0;
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-      for (int p = SPAN; p < nch; p += SPAN) {        // frames longer than one pass
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) {
-          const int c = p + k * LPF + gl;
-          v[k] = (c < nch) ? cp[c] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (p + k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-      }
-      uint32_t P = group_sum<LPF>(acc_lo + (acc_hi << 8));
-      P -= old_check;
-      s += args.payload_mult * P;                     // :92-103, iterations in closed form
-      const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));  // :105-106
-      if (gl == 0) {                                  // :108
-        fp[u + 6] = static_cast<uint8_t>(c & 0xff);
-        fp[u + 7] = static_cast<uint8_t>(c >> 8);
-      }
-    }
-    if (gl == 0) args.verdicts[f] = verdict;
-    // the next iteration rewrites this group's LDS window
-    compiler_barrier();
-    d = dn;
+    wf = wn;
   }
 }
 
@@ -229,10 +351,10 @@ DeviceInfo device_info(int dev) {
   return cache[dev];
 }
 
-template <int LPF, int NCH>
+template <int LPF, int NCH, int U>
 int launch(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   constexpr int G = kWave / LPF;
-  constexpr int frames_per_block = kWavesPerBlock * G;
+  constexpr int frames_per_block = kWavesPerBlock * G * U;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) { set_error(e, "hipGetDevice"); return -EIO; }
@@ -240,9 +362,61 @@ int launch(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   const uint32_t cap = static_cast<uint32_t>((di.ok ? di.cus : 256) * blocks_per_cu);
   const uint32_t need = (a.n + frames_per_block - 1) / frames_per_block;
   const uint32_t blocks = need < cap ? need : cap;
-  hipLaunchKernelGGL((checksum_kernel<LPF, NCH>), dim3(blocks), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL((checksum_kernel<LPF, NCH, U>), dim3(blocks), dim3(kBlock), 0, stream, a);
   e = hipGetLastError();
   if (e != hipSuccess) { set_error(e, "checksum_kernel launch"); return -EIO; }
+  return 0;
+}
+
+// Instantiated launch shapes: {lanes per frame, 16-B chunks per lane and pass,
+// frames per group and iteration}.  The default picks one by frame_len_hint.
+struct Variant {
+  int lpf, nch, u;
+  int (*fn)(const KernelArgs &, hipStream_t, int);
+};
+
+#define XSKNF_V(L, N, U) {L, N, U, &launch<L, N, U>}
+const Variant kVariants[] = {
+    XSKNF_V(8, 1, 1),  XSKNF_V(16, 1, 1), XSKNF_V(16, 1, 2), XSKNF_V(16, 2, 1), XSKNF_V(16, 2, 2),
+    XSKNF_V(32, 1, 1), XSKNF_V(32, 1, 2), XSKNF_V(32, 2, 1), XSKNF_V(32, 2, 2), XSKNF_V(32, 3, 1),
+    XSKNF_V(32, 3, 2), XSKNF_V(64, 1, 1), XSKNF_V(64, 2, 1), XSKNF_V(64, 2, 2), XSKNF_V(64, 3, 1),
+    XSKNF_V(64, 4, 1), XSKNF_V(64, 4, 2), XSKNF_V(64, 6, 1), XSKNF_V(64, 9, 1),
+};
+#undef XSKNF_V
+
+const Variant *find_variant(int lpf, int nch, int u) {
+  for (const Variant &v : kVariants)
+    if (v.lpf == lpf && v.nch == nch && v.u == u) return &v;
+  return nullptr;
+}
+
+// default shape for a length hint: one pass covers hint + 15 bytes of misalignment
+void default_shape(uint32_t hint, int &lpf, int &nch, int &u) {
+  if (hint + 15 <= 128) { lpf = 8; nch = 1; u = 1; }
+  else if (hint + 15 <= 512) { lpf = 16; nch = 2; u = 2; }
+  else if (hint + 15 <= 1536) { lpf = 32; nch = 3; u = 2; }
+  else if (hint + 15 <= 4096) { lpf = 64; nch = 4; u = 2; }
+  else { lpf = 64; nch = 9; u = 1; }
+}
+
+int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_desc *descs, uint32_t n,
+            uint32_t ingress_ifindex, const xsknf_csum_opts *opts, int32_t *verdicts) {
+  if (!opts || opts->reserved != 0) return -EINVAL;
+  if (opts->action != XSKNF_CSUM_ACTION_REDIRECT && opts->action != XSKNF_CSUM_ACTION_DROP) return -EINVAL;
+  if (opts->action == XSKNF_CSUM_ACTION_REDIRECT && opts->num_interfaces == 0) return -EINVAL;
+  if (n == 0) return 1;
+  if (!umem || !descs || !verdicts) return -EINVAL;
+  a.umem = umem;
+  a.umem_size = umem_size;
+  a.descs = descs;
+  a.verdicts = verdicts;
+  a.n = n;
+  a.payload_mult = opts->csum_iterations > 0 ? static_cast<uint32_t>(opts->csum_iterations) : 0u;
+  // aligned-down descriptor address: inside the descriptor array's own page
+  a.dummy = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(descs) & ~static_cast<uintptr_t>(15));
+  a.fwd_verdict = opts->action == XSKNF_CSUM_ACTION_REDIRECT
+                      ? static_cast<int32_t>((ingress_ifindex + 1u) % opts->num_interfaces)
+                      : -1;
   return 0;
 }
 
@@ -265,30 +439,36 @@ int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size, const struct xsk
                              uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
                              int32_t *verdicts, uint32_t frame_len_hint, void *stream) {
   using namespace xsknf_gpu;
-  if (!opts || opts->reserved != 0) return -EINVAL;
-  if (opts->action != XSKNF_CSUM_ACTION_REDIRECT && opts->action != XSKNF_CSUM_ACTION_DROP) return -EINVAL;
-  if (opts->action == XSKNF_CSUM_ACTION_REDIRECT && opts->num_interfaces == 0) return -EINVAL;
-  if (n == 0) return 0;
-  if (!umem || !descs || !verdicts) return -EINVAL;
-
   KernelArgs a;
-  a.umem = umem;
-  a.umem_size = umem_size;
-  a.descs = descs;
-  a.verdicts = verdicts;
-  a.n = n;
-  a.payload_mult = opts->csum_iterations > 0 ? static_cast<uint32_t>(opts->csum_iterations) : 0u;
-  a.fwd_verdict = opts->action == XSKNF_CSUM_ACTION_REDIRECT
-                      ? static_cast<int32_t>((ingress_ifindex + 1u) % opts->num_interfaces)
-                      : -1;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const uint32_t hint = frame_len_hint ? frame_len_hint : 2048u;
-  // size classes: one pass must cover hint + 15 bytes of 16-byte misalignment
-  if (hint + 15 <= 128) return launch<4, 2>(a, s, 8);
-  if (hint + 15 <= 512) return launch<16, 2>(a, s, 8);
-  if (hint + 15 <= 1536) return launch<32, 3>(a, s, 8);
-  if (hint + 15 <= 4096) return launch<64, 4>(a, s, 8);
-  return launch<64, 9>(a, s, 8);
+  const int rc = prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
+  if (rc != 0) return rc < 0 ? rc : 0;
+  int lpf, nch, u;
+  default_shape(frame_len_hint ? frame_len_hint : 2048u, lpf, nch, u);
+  return find_variant(lpf, nch, u)->fn(a, static_cast<hipStream_t>(stream), 8);
+}
+
+int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
+                                 uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+                                 int32_t *verdicts, const struct xsknf_gpu_launch_cfg *cfg, void *stream) {
+  using namespace xsknf_gpu;
+  if (!cfg || cfg->blocks_per_cu < 0 || cfg->blocks_per_cu > 64) return -EINVAL;
+  const Variant *v = find_variant(cfg->lanes_per_frame, cfg->chunks_per_lane, cfg->frames_per_group);
+  if (!v) return -EINVAL;
+  KernelArgs a;
+  const int rc = prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
+  if (rc != 0) return rc < 0 ? rc : 0;
+  return v->fn(a, static_cast<hipStream_t>(stream), cfg->blocks_per_cu ? cfg->blocks_per_cu : 8);
+}
+
+int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg) {
+  if (!cfg) return -EINVAL;
+  int lpf, nch, u;
+  xsknf_gpu::default_shape(frame_len_hint ? frame_len_hint : 2048u, lpf, nch, u);
+  cfg->lanes_per_frame = lpf;
+  cfg->chunks_per_lane = nch;
+  cfg->frames_per_group = u;
+  cfg->blocks_per_cu = 8;
+  return 0;
 }
 
 }  // extern "C"
