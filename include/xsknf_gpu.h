@@ -87,14 +87,18 @@ int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * `lanes_per_frame` lanes (8, 16, 32 or 64) owns one frame at a time and loads
  * `chunks_per_lane` 16-byte chunks per pass; `frames_per_group` frames have
  * their loads in flight together; the persistent grid has `blocks_per_cu`
- * 256-thread blocks per CU (0 = 8).  Only instantiated shapes are accepted
- * (-EINVAL otherwise); every shape gives identical results.
+ * 256-thread blocks per CU (0 = 8).  `lds_ring` > 0 selects the LDS-DMA
+ * kernel, which streams each wave's frames through a ring of that many LDS
+ * slots (frames_per_group is then ignored); 0 selects the register kernel.
+ * Only instantiated shapes are accepted (-EINVAL otherwise); every shape gives
+ * identical results.
  */
 struct xsknf_gpu_launch_cfg {
 	int32_t lanes_per_frame;
 	int32_t chunks_per_lane;
 	int32_t frames_per_group;
 	int32_t blocks_per_cu;
+	int32_t lds_ring;
 };
 
 /* The shape xsknf_gpu_checksum_batch() uses for a given frame_len_hint. */

@@ -45,6 +45,7 @@ class LaunchCfg(ctypes.Structure):
         ("chunks_per_lane", ctypes.c_int32),
         ("frames_per_group", ctypes.c_int32),
         ("blocks_per_cu", ctypes.c_int32),
+        ("lds_ring", ctypes.c_int32),
     ]
 
 

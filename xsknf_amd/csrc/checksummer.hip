@@ -46,11 +46,13 @@ __device__ __forceinline__ uint64_t umem_offset(uint64_t addr) {
 }
 
 // 0x01 in every byte b of the dword at window offset x with lo <= x+b < hi.
+// (bytes [a, b) of a dword, a/b clamped to 0..4: two 64-bit shifts of 0x01010101)
 __device__ __forceinline__ uint32_t byte_ones(int lo, int hi, int x) {
-  const int a = min(max(lo - x, 0), 4);
-  const int b = min(max(hi - x, 0), 4);
-  const uint64_t m = ((1ull << (8 * b)) - 1ull) & ~((1ull << (8 * a)) - 1ull);
-  return static_cast<uint32_t>(m) & 0x01010101u;
+  const int a8 = min(max(8 * (lo - x), 0), 32);
+  const int b8 = min(max(8 * (hi - x), 0), 32);
+  const uint32_t below_b = static_cast<uint32_t>((0x01010101ull << b8) >> 32);
+  const uint32_t from_a = static_cast<uint32_t>(0x01010101ull << a8);
+  return below_b & from_a;
 }
 
 // Sum of one 16-byte chunk's bytes in [lo, hi) (window offsets), split by the
@@ -325,6 +327,187 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
   }
 }
 
+// ---- LDS-DMA ring variant --------------------------------------------------
+//
+// Each wave streams its frames through a private ring of R slots in LDS filled
+// by global_load_lds_dwordx4 (LDS-DMA: 16 B per lane straight into LDS, no VGPR
+// destination).  At step i the wave issues the DMA of step i+R-1 and then waits
+// -- with an explicitly counted vmcnt -- only for step i's slot, so R-1 steps of
+// loads stay in flight while step i is parsed, summed and reduced, and the
+// loads cost no registers (occupancy stays high).  The DMA is issued from
+// inline asm because the compiler drains vmcnt to 0 before every LDS read once
+// it sees an LDS-DMA in flight; the waits here count only this wave's own DMAs
+// that are younger than the slot being read (other vector-memory operations
+// can only make the wait stricter, never too weak).
+//
+// Slot layout: DMA instruction k of a step writes 1 KiB at slot + k*1024, lane l
+// at +16*l, so group g's chunk c = k*LPF + gl sits at slot + k*1024 + g*LPF*16 +
+// gl*16, and chunks 0..LPF-1 of a frame (bytes [0, 16*LPF - rs) of the frame,
+// every header byte for LPF >= 8) are contiguous at slot + g*LPF*16.
+
+__device__ __forceinline__ void dma16(const void *gaddr, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(gaddr), "s"(lds_addr) : "memory", "m0");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx950");
+  asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_u32(uint32_t addr) {
+  // may be unaligned: gfx950 LDS serves unaligned dword reads
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(static_cast<uintptr_t>(addr));
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 lds_u128(uint32_t addr) {
+  const u32x4 x = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(static_cast<uintptr_t>(addr));
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+// Group sum via DPP: the total lands in the group's LAST lane (lane LPF-1).
+template <int LPF>
+__device__ __forceinline__ uint32_t group_sum_last(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  if constexpr (LPF >= 16) v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  if constexpr (LPF >= 32) v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+  if constexpr (LPF >= 64) v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+  return v;
+}
+
+// Issue the NCH DMAs of one frame window per group into `slot` (chunk index
+// clamped into the window, as in load_pass).
+template <int LPF, int NCH>
+__device__ __forceinline__ void dma_pass(const FrameRef &r, int gl, uint32_t slot) {
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = min(k * LPF + gl, r.nch - 1);
+    dma16(r.cp + c, slot + k * 1024);
+  }
+}
+
+// Parse + sum + reduce one frame per group from a landed slot; returns the
+// frame's stores (issued by the group's last lane).
+template <int LPF, int NCH>
+__device__ __forceinline__ void process_slot(const KernelArgs &args, const FrameRef &r, uint32_t f,
+                                             uint32_t slot, int grp, int gl, int lane) {
+  constexpr int SPAN = LPF * NCH;
+  const uint32_t hb = slot + grp * LPF * 16 + r.rs;        // frame byte i at hb + i
+  const uint32_t w12 = lds_u32(hb + 12);                   // f[12..15]
+  const uint32_t w20 = lds_u32(hb + 20);                   // f[20..23]
+  const uint32_t w24 = lds_u32(hb + 24);                   // f[24..27]
+  const uint32_t w28 = lds_u32(hb + 28);                   // f[28..31]
+  const uint32_t w32 = lds_u32(hb + 32);                   // f[32..35]
+  const int u = 14 + 4 * ((w12 >> 16) & 0x0f);             // :52, ihl unvalidated
+  const uint32_t wu = lds_u32(hb + u + 4);                 // f[u+4..u+7]: udp len, old check
+  uint4 v[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) v[k] = lds_u128(slot + k * 1024 + lane * 16);
+
+  const bool ipv4 = (w12 & 0xffffu) == 0x0008u;           // f[12..13] == 08 00
+  const bool udp = (w20 >> 24) == 17u;                     // f[23]
+  int32_t verdict;
+  bool do_sum = false;
+  if (!r.live) {
+    verdict = -1;                                   // :34-37 (and out-of-range descriptors)
+  } else if (!ipv4) {
+    verdict = 0;                                    // :39-41
+  } else if (r.len < 34) {
+    verdict = -1;                                   // :43-46
+  } else if (!udp) {
+    verdict = 0;                                    // :48-50
+  } else if (u + 8 > r.len) {
+    verdict = -1;                                   // :53-55
+  } else {
+    verdict = args.fwd_verdict;                     // :110-111
+    do_sum = true;
+  }
+
+  const int lo = r.rs + u;
+  const int hi = r.rs + r.len;
+  const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+  const uint32_t wh = wl << 8 | wl >> 24;
+  uint32_t acc_lo = 0, acc_hi = 0;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+  if (do_sum) {
+    for (int p = SPAN; p < r.nch; p += SPAN) {      // frames longer than one pass: direct loads
+      uint4 t[NCH];
+      load_pass<LPF, NCH>(r, p, gl, t);
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) chunk_sum(t[k], (p + k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+    }
+  }
+  const uint32_t P = group_sum_last<LPF>(acc_lo + (acc_hi << 8)) - (wu >> 16);   // old check counted as 0 (:68)
+  if (gl == LPF - 1 && r.exists) {
+    if (do_sum) {
+      // :57-65 pseudo-header: le16(26) + le16(28) + le16(30) + le16(32) + 17<<8 + le16(u+4)
+      uint32_t s = (w24 >> 16) + (w28 & 0xffffu) + (w28 >> 16) + (w32 & 0xffffu) + 0x1100u + (wu & 0xffffu);
+      s += args.payload_mult * P;                   // :92-103, iterations in closed form
+      const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));  // :105-106
+      *reinterpret_cast<uint16_t *>(r.fp + u + 6) = c;   // :108
+    }
+    args.verdicts[f] = verdict;
+  }
+}
+
+template <int LPF, int NCH, int R>
+__global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs args) {
+  static_assert(kWave % LPF == 0 && LPF >= 8, "header window must sit in chunk slot k = 0");
+  static_assert(R >= 2 && R <= 4, "ring depth");
+  static_assert((R - 1) * NCH < 64, "vmcnt range");
+  constexpr int G = kWave / LPF;
+  constexpr int SLOT = NCH * 1024;
+  static_assert(G <= 8, "descriptor prefetch is held in SGPRs");
+
+  __shared__ __attribute__((aligned(1024))) uint8_t ring[kWavesPerBlock][R][SLOT];
+
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int grp = lane / LPF;
+  const int gl = lane % LPF;
+  const uint32_t ring0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(&ring[wv][0][0]));
+  const uint32_t wstride = gridDim.x * kWavesPerBlock * G;
+  const uint32_t last = args.n - 1;
+  const uint32_t w0 = (blockIdx.x * kWavesPerBlock + wv) * G;
+
+  // frames of step j of this wave: w0 + j * wstride + grp
+  FrameRef ref[R];
+  // prologue: steps 0 .. R-2 in flight
+#pragma unroll
+  for (int j = 0; j < R - 1; ++j) {
+    const uint32_t wf = w0 + j * wstride;
+    ref[j] = make_ref(args, pick<G>(load_descs<G>(args, wf, last), grp), wf + grp < args.n);
+    dma_pass<LPF, NCH>(ref[j], gl, ring0 + j * SLOT);
+  }
+  DescSet<G> dpre = load_descs<G>(args, w0 + (R - 1) * wstride, last);
+
+  // Unrolled by R so ring slots and the per-step FrameRefs are static.
+  uint32_t wf = w0;
+  while (true) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      if (wf >= args.n) {        // wave-uniform exit; drain this wave's DMAs first
+        wait_vmcnt<0>();
+        return;
+      }
+      const int sn = (s + R - 1) % R;                  // slot of step i+R-1 (freed by step i-1)
+      const uint32_t wn = wf + (R - 1) * wstride;
+      ref[sn] = make_ref(args, pick<G>(dpre, grp), wn + grp < args.n);
+      dpre = load_descs<G>(args, wn + wstride, last);
+      dma_pass<LPF, NCH>(ref[sn], gl, ring0 + sn * SLOT);
+      wait_vmcnt<(R - 1) * NCH>();                     // step i's slot has landed
+      process_slot<LPF, NCH>(args, ref[s], wf + grp, ring0 + s * SLOT, grp, gl, lane);
+      wf += wstride;
+    }
+  }
+}
+
 // ---- host side -------------------------------------------------------------
 
 thread_local char g_last_error[256] = "";
@@ -368,25 +551,47 @@ int launch(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return 0;
 }
 
+template <int LPF, int NCH, int R>
+int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
+  constexpr int G = kWave / LPF;
+  constexpr int frames_per_block = kWavesPerBlock * G;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) { set_error(e, "hipGetDevice"); return -EIO; }
+  const DeviceInfo di = device_info(dev);
+  const uint32_t cap = static_cast<uint32_t>((di.ok ? di.cus : 256) * blocks_per_cu);
+  const uint32_t need = (a.n + frames_per_block - 1) / frames_per_block;
+  const uint32_t blocks = need < cap ? need : cap;
+  hipLaunchKernelGGL((checksum_kernel_dma<LPF, NCH, R>), dim3(blocks), dim3(kBlock), 0, stream, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) { set_error(e, "checksum_kernel_dma launch"); return -EIO; }
+  return 0;
+}
+
 // Instantiated launch shapes: {lanes per frame, 16-B chunks per lane and pass,
 // frames per group and iteration}.  The default picks one by frame_len_hint.
 struct Variant {
-  int lpf, nch, u;
+  int lpf, nch, u, ring;
   int (*fn)(const KernelArgs &, hipStream_t, int);
 };
 
-#define XSKNF_V(L, N, U) {L, N, U, &launch<L, N, U>}
+#define XSKNF_V(L, N, U) {L, N, U, 0, &launch<L, N, U>}
+#define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
 const Variant kVariants[] = {
     XSKNF_V(8, 1, 1),  XSKNF_V(16, 1, 1), XSKNF_V(16, 1, 2), XSKNF_V(16, 2, 1), XSKNF_V(16, 2, 2),
     XSKNF_V(32, 1, 1), XSKNF_V(32, 1, 2), XSKNF_V(32, 2, 1), XSKNF_V(32, 2, 2), XSKNF_V(32, 3, 1),
     XSKNF_V(32, 3, 2), XSKNF_V(64, 1, 1), XSKNF_V(64, 2, 1), XSKNF_V(64, 2, 2), XSKNF_V(64, 3, 1),
     XSKNF_V(64, 4, 1), XSKNF_V(64, 4, 2), XSKNF_V(64, 6, 1), XSKNF_V(64, 9, 1),
+    XSKNF_D(8, 1, 3),  XSKNF_D(8, 1, 4),  XSKNF_D(16, 1, 3), XSKNF_D(16, 2, 3), XSKNF_D(32, 2, 3),
+    XSKNF_D(32, 3, 2), XSKNF_D(32, 3, 3), XSKNF_D(64, 2, 3), XSKNF_D(64, 2, 4), XSKNF_D(64, 3, 3),
+    XSKNF_D(64, 4, 2), XSKNF_D(64, 4, 3),
 };
 #undef XSKNF_V
+#undef XSKNF_D
 
-const Variant *find_variant(int lpf, int nch, int u) {
+const Variant *find_variant(int lpf, int nch, int u, int ring) {
   for (const Variant &v : kVariants)
-    if (v.lpf == lpf && v.nch == nch && v.u == u) return &v;
+    if (v.lpf == lpf && v.nch == nch && v.ring == ring && (ring || v.u == u)) return &v;
   return nullptr;
 }
 
@@ -444,7 +649,7 @@ int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size, const struct xsk
   if (rc != 0) return rc < 0 ? rc : 0;
   int lpf, nch, u;
   default_shape(frame_len_hint ? frame_len_hint : 2048u, lpf, nch, u);
-  return find_variant(lpf, nch, u)->fn(a, static_cast<hipStream_t>(stream), 8);
+  return find_variant(lpf, nch, u, 0)->fn(a, static_cast<hipStream_t>(stream), 8);
 }
 
 int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
@@ -452,7 +657,8 @@ int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct
                                  int32_t *verdicts, const struct xsknf_gpu_launch_cfg *cfg, void *stream) {
   using namespace xsknf_gpu;
   if (!cfg || cfg->blocks_per_cu < 0 || cfg->blocks_per_cu > 64) return -EINVAL;
-  const Variant *v = find_variant(cfg->lanes_per_frame, cfg->chunks_per_lane, cfg->frames_per_group);
+  const Variant *v = find_variant(cfg->lanes_per_frame, cfg->chunks_per_lane, cfg->frames_per_group,
+                                  cfg->lds_ring);
   if (!v) return -EINVAL;
   KernelArgs a;
   const int rc = prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
@@ -468,6 +674,7 @@ int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launc
   cfg->chunks_per_lane = nch;
   cfg->frames_per_group = u;
   cfg->blocks_per_cu = 8;
+  cfg->lds_ring = 0;
   return 0;
 }
 
