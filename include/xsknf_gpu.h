@@ -90,8 +90,11 @@ int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * 256-thread blocks per CU (0 = 8).  `lds_ring` > 0 selects the LDS-DMA
  * kernel, which streams each wave's frames through a ring of that many LDS
  * slots (frames_per_group is then ignored); 0 selects the register kernel.
- * Only instantiated shapes are accepted (-EINVAL otherwise); every shape gives
- * identical results.
+ * `fused_stores` = 1 writes the check bytes from the summing kernel itself;
+ * 0 (default) parks them and writes them in a second, write-only pass, which is
+ * faster on MI355X (scattered writes mixed into the read stream cost ~25 % of
+ * the read bandwidth).  Only instantiated shapes are accepted (-EINVAL
+ * otherwise); every shape gives identical results.
  */
 struct xsknf_gpu_launch_cfg {
 	int32_t lanes_per_frame;
@@ -99,6 +102,7 @@ struct xsknf_gpu_launch_cfg {
 	int32_t frames_per_group;
 	int32_t blocks_per_cu;
 	int32_t lds_ring;
+	int32_t fused_stores;
 };
 
 /* The shape xsknf_gpu_checksum_batch() uses for a given frame_len_hint. */

@@ -168,3 +168,40 @@ def test_full_size_configs_bit_exact(dev, name, n, length, layout):
     assert np.array_equal(umem.cpu().numpy(), host_in)
     # every synthetic frame is a valid UDP frame: all REDIRECT to iface 0
     assert (gv == 0).all()
+
+
+SHAPES = [
+    # lanes_per_frame, chunks_per_lane, frames_per_group, lds_ring, fused_stores
+    (8, 1, 1, 0, 0), (8, 1, 1, 0, 1), (16, 2, 2, 0, 0), (32, 3, 2, 0, 1), (32, 3, 2, 0, 0),
+    (64, 9, 1, 0, 0), (8, 1, 1, 3, 0), (16, 2, 1, 3, 1), (32, 3, 1, 2, 0), (32, 3, 1, 3, 1),
+    (64, 4, 1, 3, 0), (64, 2, 1, 4, 1),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=["-".join(map(str, s)) for s in SHAPES])
+@pytest.mark.parametrize("layout", ["aligned", "unaligned"])
+def test_every_launch_shape_is_bit_exact(dev, shape, layout):
+    """Each kernel family / shape / store mode, through xsknf_gpu_checksum_batch_cfg."""
+    import ctypes
+    from xsknf_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(sum(shape))
+    lens = rng.integers(0, 3000, size=2500).astype(np.uint32)
+    if layout == "aligned":
+        b = frames.aligned_batch(2500, np.minimum(lens, 1792), chunk=2048, seed=sum(shape))
+    else:
+        b = frames.unaligned_batch(2500, lens, seed=sum(shape))
+    frames.inject_edge_cases(b, 0.1)
+    ou, ov = run_oracle(b, iters=2, action=O.REDIRECT, nif=3, ingress=1)
+    umem = torch.from_numpy(b.umem).to(dev)
+    descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+    v = torch.empty(b.n, dtype=torch.int32, device=dev)
+    cfg = _lib.LaunchCfg(shape[0], shape[1], shape[2], 4, shape[3], shape[4])
+    rc = lib.xsknf_gpu_checksum_batch_cfg(
+        ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), b.n, 1,
+        ctypes.byref(_lib.CsumOpts(2, O.REDIRECT, 3, 0)), ctypes.c_void_p(v.data_ptr()),
+        ctypes.byref(cfg), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), ov)
+    assert np.array_equal(umem.cpu().numpy(), ou)

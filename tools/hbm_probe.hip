@@ -5,7 +5,11 @@
 // For n chunks of `stride` bytes, read bytes [off, off+len) of every chunk with
 // 16-byte loads (len rounded up to 16), flat-indexed over all (chunk, 16-B
 // piece) pairs, 4 loads in flight per lane, and report GB/s of the bytes read.
-//   hbm_probe <total_chunks> <stride> <off> <len> [reps]
+//   hbm_probe <total_chunks> <stride> <off> <len> [reps] [wr_check] [wr_verdict]
+// wr_check / wr_verdict add the checksummer's own stores: 2 bytes at frame
+// byte 40 of every chunk (in place) / one 4-byte verdict per chunk;
+// wr_check = 16/32/64/128 instead rewrites the whole aligned block of that size
+// around frame byte 40 with 16-byte stores.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -14,9 +18,10 @@
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
 
-__global__ __launch_bounds__(256) void probe(const uint8_t *__restrict__ base, uint64_t pieces,
+__global__ __launch_bounds__(256) void probe(uint8_t *__restrict__ base, uint64_t pieces,
                                              uint32_t ppc, uint32_t stride, uint32_t off,
-                                             uint32_t *__restrict__ out) {
+                                             uint32_t *__restrict__ out, int wr_check, int wr_verdict,
+                                             uint32_t *__restrict__ verdicts) {
   uint32_t acc = 0;
   const uint64_t tid = blockIdx.x * 256ull + threadIdx.x;
   const uint64_t nthr = gridDim.x * 256ull;
@@ -30,9 +35,33 @@ __global__ __launch_bounds__(256) void probe(const uint8_t *__restrict__ base, u
       v[k] = *reinterpret_cast<const uint4 *>(base + c * stride + off + p * 16);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    for (int k = 0; k < 4; ++k) {
+      acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+      const uint64_t j = i + k * nthr;
+      if (j < pieces) {
+        const uint64_t c = j / ppc, p = j % ppc;
+        // the checksummer's stores: 2 bytes at frame byte 40 (piece 2), 4 B verdict (piece 0)
+        if (wr_check == 1 && p == 2) *reinterpret_cast<uint16_t *>(base + c * stride + off + 40) = (uint16_t)v[k].x;
+        // wr_check = B > 1: rewrite the whole aligned B-byte block holding frame byte 40
+        if (wr_check > 1) {
+          const uint64_t a = c * stride + off + 40;
+          const uint64_t blk = a & ~(uint64_t)(wr_check - 1);
+          const uint64_t me = c * stride + off + p * 16;
+          if (me >= blk && me < blk + wr_check) *reinterpret_cast<uint4 *>(base + me) = v[k];
+        }
+        if (wr_verdict && p == 0) verdicts[c] = v[k].y;
+      }
+    }
   }
   if (acc == 0x12345678u) out[0] = acc;   // keeps the loads live
+}
+
+// write-only pass: every chunk gets 2 bytes at byte off+40 from a compact u32 array
+__global__ __launch_bounds__(256) void scatter(uint8_t *__restrict__ base, uint64_t chunks,
+                                               uint32_t stride, uint32_t off,
+                                               const uint32_t *__restrict__ vals) {
+  for (uint64_t c = blockIdx.x * 256ull + threadIdx.x; c < chunks; c += gridDim.x * 256ull)
+    *reinterpret_cast<uint16_t *>(base + c * stride + off + 40) = (uint16_t)vals[c];
 }
 
 int main(int argc, char **argv) {
@@ -40,10 +69,13 @@ int main(int argc, char **argv) {
   const uint64_t chunks = strtoull(argv[1], 0, 0);
   const uint32_t stride = atoi(argv[2]), off = atoi(argv[3]), len = atoi(argv[4]);
   const int reps = argc > 5 ? atoi(argv[5]) : 20;
+  const int wr_check = argc > 6 ? atoi(argv[6]) : 0;
+  const int wr_verdict = argc > 7 ? atoi(argv[7]) : 0;
   const uint32_t ppc = (len + 15) / 16;
   const uint64_t bytes = chunks * stride + 64;
   uint8_t *buf;
-  uint32_t *out;
+  uint32_t *out, *verdicts;
+  CHECK(hipMalloc(&verdicts, chunks * 4));
   CHECK(hipMalloc(&buf, bytes));
   CHECK(hipMalloc(&out, 4));
   CHECK(hipMemset(buf, 1, bytes));
@@ -54,16 +86,26 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(probe, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(probe, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out, wr_check, wr_verdict, verdicts);
   CHECK(hipEventRecord(e0));
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(probe, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(probe, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out, wr_check, wr_verdict, verdicts);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / reps;
+  if (getenv("PROBE_SCATTER")) {
+    CHECK(hipEventRecord(e0));
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(scatter, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms2 = 0;
+    CHECK(hipEventElapsedTime(&ms2, e0, e1));
+    printf("{\"scatter_only_us\": %.2f, \"chunks\": %llu, \"stride\": %u}\n", ms2 * 1e3 / reps,
+           (unsigned long long)chunks, stride);
+  }
   const double rd = (double)pieces * 16;
-  printf("{\"chunks\": %llu, \"stride\": %u, \"off\": %u, \"len\": %u, \"us\": %.2f, \"read_GBps\": %.1f}\n",
-         (unsigned long long)chunks, stride, off, len, us, rd / us / 1e3);
+  printf("{\"chunks\": %llu, \"stride\": %u, \"off\": %u, \"len\": %u, \"wr_check\": %d, \"wr_verdict\": %d, \"us\": %.2f, \"read_GBps\": %.1f}\n",
+         (unsigned long long)chunks, stride, off, len, wr_check, wr_verdict, us, rd / us / 1e3);
   return 0;
 }

@@ -46,6 +46,7 @@ class LaunchCfg(ctypes.Structure):
         ("frames_per_group", ctypes.c_int32),
         ("blocks_per_cu", ctypes.c_int32),
         ("lds_ring", ctypes.c_int32),
+        ("fused_stores", ctypes.c_int32),
     ]
 
 
