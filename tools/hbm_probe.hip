@@ -56,6 +56,48 @@ __global__ __launch_bounds__(256) void probe(uint8_t *__restrict__ base, uint64_
   if (acc == 0x12345678u) out[0] = acc;   // keeps the loads live
 }
 
+// read variants: mode 1 = register loads with the nt (non-temporal) policy,
+// mode 2 = LDS-DMA (global_load_lds_dwordx4) default policy, mode 3 = LDS-DMA nt
+template <int MODE>
+__global__ __launch_bounds__(256) void probe_mode(const uint8_t *__restrict__ base, uint64_t pieces,
+                                                  uint32_t ppc, uint32_t stride, uint32_t off,
+                                                  uint32_t *__restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t sink[4][4][1024];
+  uint32_t acc = 0;
+  const uint64_t tid = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t nthr = gridDim.x * 256ull;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  for (uint64_t i = tid; i < pieces; i += 4 * nthr) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t j = i + k * nthr;
+      const uint64_t jj = j < pieces ? j : pieces - 1;
+      const uint64_t c = jj / ppc, p = jj % ppc;
+      const uint8_t *a = base + c * stride + off + p * 16;
+      if (MODE == 1) {
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        const u4v x = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a));
+        v[k] = make_uint4(x.x, x.y, x.z, x.w);
+      } else {
+        const uint32_t l = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(&sink[wv][k][0]));
+        if (MODE == 2)
+          asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(a), "s"(l) : "memory", "m0");
+        else
+          asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" :: "v"(a), "s"(l) : "memory", "m0");
+      }
+    }
+    if (MODE == 1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    } else {
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // keep two groups in flight
+    }
+  }
+  if (MODE != 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 // write-only pass: every chunk gets 2 bytes at byte off+40 from a compact u32 array
 __global__ __launch_bounds__(256) void scatter(uint8_t *__restrict__ base, uint64_t chunks,
                                                uint32_t stride, uint32_t off,
@@ -94,6 +136,24 @@ int main(int argc, char **argv) {
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / reps;
+  const double rd = (double)pieces * 16;
+  if (getenv("PROBE_MODES")) {
+    for (int m = 1; m <= 3; ++m) {
+      CHECK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r) {
+        if (m == 1) hipLaunchKernelGGL(probe_mode<1>, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out);
+        if (m == 2) hipLaunchKernelGGL(probe_mode<2>, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out);
+        if (m == 3) hipLaunchKernelGGL(probe_mode<3>, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out);
+      }
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms2 = 0;
+      CHECK(hipEventElapsedTime(&ms2, e0, e1));
+      const double us2 = ms2 * 1e3 / reps;
+      printf("{\"mode\": \"%s\", \"len\": %u, \"us\": %.2f, \"read_GBps\": %.1f}\n",
+             m == 1 ? "reg_nt" : (m == 2 ? "ldsdma" : "ldsdma_nt"), len, us2, rd / us2 / 1e3);
+    }
+  }
   if (getenv("PROBE_SCATTER")) {
     CHECK(hipEventRecord(e0));
     for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(scatter, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
@@ -104,7 +164,6 @@ int main(int argc, char **argv) {
     printf("{\"scatter_only_us\": %.2f, \"chunks\": %llu, \"stride\": %u}\n", ms2 * 1e3 / reps,
            (unsigned long long)chunks, stride);
   }
-  const double rd = (double)pieces * 16;
   printf("{\"chunks\": %llu, \"stride\": %u, \"off\": %u, \"len\": %u, \"wr_check\": %d, \"wr_verdict\": %d, \"us\": %.2f, \"read_GBps\": %.1f}\n",
          (unsigned long long)chunks, stride, off, len, wr_check, wr_verdict, us, rd / us / 1e3);
   return 0;

@@ -1,34 +1,43 @@
-// checksummer.hip -- gfx950 kernel for the xsknf checksummer per-packet path.
+// checksummer.hip -- gfx950 kernels for the xsknf checksummer per-packet path.
 //
 // Reference semantics: examples/checksummer/checksummer_user.c:30-112
 // (xsknf_packet_processor), applied to every descriptor of an rx batch as the
 // per-frame loop of src/xsknf.c:654-672 does.
 //
-// The reference sums 16-bit words serially from the UDP header to the end of
-// the frame.  The sum is a wrapping u32, so it can be taken in any order and
-// in closed form:
+// Arithmetic.  The reference sums 16-bit words serially from the UDP header to
+// the end of the frame into a wrapping u32, so the sum can be taken in any
+// order and in closed form:
 //     s = pseudo + max(iters,0) * P                         (mod 2^32)
 //     P = sum_{k even} f[u+k] + 256 * sum_{k odd} f[u+k],   k in [0, len-u)
-// with f[u+6], f[u+7] (the old check) counted as zero.  "k even" is the set of
-// bytes whose ABSOLUTE address parity equals that of the UDP header start, so
-// the kernel reads the frame as 16-byte aligned chunks wherever the frame
-// starts (unaligned-chunk UMEM puts frames at odd addresses) and splits every
-// dword into its low-weight and high-weight byte pairs with v_dot4_u32_u8,
-// whose u8 weight operand also carries the [udp, end) byte mask.
+// with f[u+6], f[u+7] (the old check) counted as zero.  "k even" are the bytes
+// whose ABSOLUTE address parity equals that of the UDP header start, so frames
+// are read as 16-byte aligned chunks wherever they start (unaligned-chunk UMEM
+// puts frames at odd addresses) and every dword is split into its low- and
+// high-weight byte pairs by v_dot4_u32_u8, whose u8 weight operand also carries
+// the [udp, end) byte mask.  One fold with the carry dropped, as :105-106.
 //
-// Mapping (MI355X: 64-lane waves, HBM-bound, no MFMA): a group of LPF lanes
-// owns one frame; a wave holds 64/LPF groups; each lane loads NCH 16-byte
-// chunks per pass, so a pass covers LPF*NCH*16 contiguous bytes of the frame
-// with dwordx4 loads that are contiguous across the group's lanes.  The first
-// 7 chunks (bytes [0,112) of the aligned window, i.e. every header byte the
-// reference reads, wherever the frame starts) are staged in LDS once so the
-// parse reads bytes by address.  Group partial sums are reduced with DPP
-// shuffles; one lane per group writes the 2 check bytes and the verdict.
-// The grid is persistent (a few blocks per CU) and strides over frames, with
-// the next descriptor prefetched while the current frame's loads are in flight.
+// Mapping (MI355X: 64-lane waves, HBM-bound integer reduction, no MFMA).
+// * A group of LPF lanes owns one frame; a wave holds G = 64/LPF groups; each
+//   lane covers NCH 16-byte chunks per pass, so one pass reads LPF*NCH*16
+//   contiguous bytes of a frame with dwordx4 loads contiguous across the group.
+// * Waves own TILES of 64 consecutive frames (persistent grid striding over
+//   tiles), so per-frame results collect in LDS and leave as one 256-B store.
+// * Loads are non-temporal (streamed once; +8-10 % read bandwidth measured).
+// * Two kernel families, same results:
+//     - register: each step loads U frames per group into VGPRs, then parses /
+//       sums / reduces them one by one (frame u+1 in flight behind frame u);
+//     - LDS-DMA ring: each wave streams frames through R LDS slots filled by
+//       global_load_lds_dwordx4; R-1 steps stay in flight at no VGPR cost.
+// * Group partial sums reduce with DPP (row_shr / row_bcast) into the group's
+//   last lane.
+// * Stores are two-phase by default: the summing pass never writes the UMEM
+//   (scattered writes mixed into the read stream cost ~25 % of its bandwidth,
+//   tools/hbm_probe), it parks check records in `verdicts`; a write-only
+//   scatter pass then writes the 2 check bytes per frame and the verdicts.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <errno.h>
+#include <stdio.h>
 #include <string.h>
 
 #include "../../include/xsknf_gpu.h"
@@ -38,15 +47,59 @@ namespace xsknf_gpu {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kHdrChunks = 7;   // window chunks 0..6 hold frame bytes [0, 97) at any 16-byte phase
-constexpr int kSlotBytes = 128; // per-frame LDS slot: 16 B lead-in (shift by -rs) + 7 chunks
+constexpr int kTile = 64;        // consecutive frames per wave tile (one 256-B result store)
+constexpr int kHdrChunks = 7;    // window chunks 0..6 hold frame bytes [0, 97) at any 16-B phase
+constexpr int kSlotBytes = 128;  // register kernel: per-group LDS header window
+
+// ---- small device helpers ---------------------------------------------------
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 __device__ __forceinline__ uint64_t umem_offset(uint64_t addr) {
   return (addr & XSKNF_GPU_UNALIGNED_BUF_ADDR_MASK) + (addr >> XSKNF_GPU_UNALIGNED_BUF_OFFSET_SHIFT);
 }
 
-// 0x01 in every byte b of the dword at window offset x with lo <= x+b < hi.
-// (bytes [a, b) of a dword, a/b clamped to 0..4: two 64-bit shifts of 0x01010101)
+__device__ __forceinline__ void compiler_barrier() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p));
+}
+
+// may be unaligned: gfx950 LDS serves unaligned dword reads
+__device__ __forceinline__ uint32_t lds_u32(uint32_t a) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(static_cast<uintptr_t>(a));
+}
+
+__device__ __forceinline__ uint4 lds_u128(uint32_t a) {
+  const u32x4 x = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(static_cast<uintptr_t>(a));
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+__device__ __forceinline__ void lds_store_u128(uint32_t a, uint4 v) {
+  u32x4 x = {v.x, v.y, v.z, v.w};
+  *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(static_cast<uintptr_t>(a)) = x;
+}
+
+__device__ __forceinline__ void lds_store_i32(uint32_t a, int32_t v) {
+  *reinterpret_cast<__attribute__((address_space(3))) int32_t *>(static_cast<uintptr_t>(a)) = v;
+}
+
+__device__ __forceinline__ int32_t lds_i32(uint32_t a) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) int32_t *>(static_cast<uintptr_t>(a));
+}
+
+// non-temporal 16-byte global load (streamed once)
+__device__ __forceinline__ uint4 load_nt(const uint4 *p) {
+  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+// 0x01 in every byte b of the dword at window offset x with lo <= x+b < hi
+// (bytes [a, b) of a dword, a/b clamped to 0..4: two 64-bit shifts of 0x01010101).
 __device__ __forceinline__ uint32_t byte_ones(int lo, int hi, int x) {
   const int a8 = min(max(8 * (lo - x), 0), 32);
   const int b8 = min(max(8 * (hi - x), 0), 32);
@@ -55,8 +108,8 @@ __device__ __forceinline__ uint32_t byte_ones(int lo, int hi, int x) {
   return below_b & from_a;
 }
 
-// Sum of one 16-byte chunk's bytes in [lo, hi) (window offsets), split by the
-// weight classes wl (bytes that are low in their 16-bit word) / wh (high).
+// Bytes of one 16-byte chunk inside [lo, hi) (window offsets), summed by weight
+// class: wl = bytes low in their 16-bit word, wh = high.
 __device__ __forceinline__ void chunk_sum(const uint4 v, int x, int lo, int hi, uint32_t wl,
                                           uint32_t wh, uint32_t &acc_lo, uint32_t &acc_hi) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -68,20 +121,19 @@ __device__ __forceinline__ void chunk_sum(const uint4 v, int x, int lo, int hi, 
   }
 }
 
-__device__ __forceinline__ void compiler_barrier() {
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-}
-
+// Group sum via DPP (all lanes active): the total lands in the group's LAST lane.
 template <int LPF>
-__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
-#pragma unroll
-  for (int m = LPF / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+__device__ __forceinline__ uint32_t group_sum_last(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  if constexpr (LPF >= 8) v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  if constexpr (LPF >= 16) v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  if constexpr (LPF >= 32) v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+  if constexpr (LPF >= 64) v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
   return v;
 }
 
-// write-only sink for the unconditional stores of frames that write nothing
-__device__ uint32_t g_sink[4];
+// ---- kernel arguments, frame references, descriptors -----------------------
 
 struct KernelArgs {
   uint8_t *umem;
@@ -91,28 +143,19 @@ struct KernelArgs {
   uint32_t n;
   uint32_t payload_mult;   // max(csum_iterations, 0)
   int32_t fwd_verdict;     // REDIRECT ? (ingress+1) % n_if : -1
-  const uint4 *dummy;      // readable 16-byte block for frames that need no bytes
   uint32_t defer;          // 1: park check records in `verdicts`, scatter in a 2nd pass
+  const uint4 *dummy;      // readable 16-byte block for frames that need no bytes
 };
 
-// Two-phase stores.  Rewriting 2 bytes in every frame WHILE the frames stream
-// in costs ~25 % of the read bandwidth on MI355X (1M scattered writes mixed into
-// the read stream; measured with tools/hbm_probe: 270 -> 346 us at 1500 B),
-// while the same writes as a separate write-only pass take ~15 us.  So phase 1
-// only reads the UMEM and parks, per frame, either its final verdict or a check
-// record in verdicts[f]; phase 2 (scatter_checks) writes the check bytes and
-// the final verdict.  Records are tagged 01 in bits 31..30, which no verdict
-// (-1 or 0..XSKNF_MAX_INTERFACES-1) has.
+// Check record parked in verdicts[f] by the summing pass (two-phase stores):
+// tag 01 in bits 31..30 (no verdict, -1 or 0..XSKNF_MAX_INTERFACES-1, has it),
+// u in bits 22..16, the new check in bits 15..0.
 constexpr uint32_t kRecTag = 0x40000000u;
 constexpr uint32_t kRecTagMask = 0xC0000000u;
 
-__device__ __forceinline__ int32_t make_record(int u, uint32_t check) {
-  return static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(u) << 16) | (check & 0xffffu));
-}
-
 // Where a frame's bytes are and which 16-byte chunks cover them.  Frames that
 // need no bytes (len < 14, or a descriptor outside the UMEM) point at a dummy
-// 16-byte block so that every chunk load of the pipeline can be unconditional.
+// 16-byte block so that every chunk load can be unconditional.
 struct FrameRef {
   const uint4 *cp;   // 16-byte aligned window start (cp <= fp)
   uint8_t *fp;       // first byte of the frame
@@ -123,10 +166,9 @@ struct FrameRef {
   bool live;         // exists, in range and len >= 14
 };
 
-__device__ __forceinline__ FrameRef make_ref(const KernelArgs &a, const xsknf_gpu_desc &d, bool exists) {
+__device__ __forceinline__ FrameRef make_ref(const KernelArgs &a, uint64_t addr, uint32_t len, bool exists) {
   FrameRef r;
-  const uint64_t off = umem_offset(d.addr);
-  const uint32_t len = d.len;
+  const uint64_t off = umem_offset(addr);
   const bool in_range = off <= a.umem_size && len <= a.umem_size - off;
   r.exists = exists;
   r.live = exists && in_range && len >= 14;
@@ -145,225 +187,187 @@ __device__ __forceinline__ FrameRef make_ref(const KernelArgs &a, const xsknf_gp
   return r;
 }
 
-// Issue this lane's NCH chunk loads of pass `p0` (chunk index clamped into the
-// window: lanes past the end re-read the last chunk, which costs no HBM bytes
-// and keeps the loads free of branches so the next frame's loads stay in
-// flight while the current frame is reduced).
-template <int LPF, int NCH>
-__device__ __forceinline__ void load_pass(const FrameRef &r, int p0, int gl, uint4 (&v)[NCH]) {
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int c = min(p0 + k * LPF + gl, r.nch - 1);
-    v[k] = r.cp[c];
-  }
+// Descriptors travel per tile: the 64 descriptors of a tile (1 KiB, contiguous)
+// are staged in LDS once, and each group reads its frame's descriptor there.
+__device__ __forceinline__ FrameRef ref_from_lds(const KernelArgs &a, uint32_t dslot, uint32_t f) {
+  const uint4 d = lds_u128(dslot);          // {addr lo, addr hi, len, options}
+  return make_ref(a, (static_cast<uint64_t>(d.y) << 32) | d.x, d.z, f < a.n);
 }
 
-// The two stores a frame produces (check bytes, verdict).  They are issued at
-// the start of the NEXT step, before that step's loads, and by every lane
-// unconditionally (lanes of a group write identical values to one address;
-// frames with nothing to write aim at a sink word).  No store then sits
-// between a frame's loads and their use, nor inside a branch, so the compiler
-// can wait for exactly the loads it needs instead of draining vmcnt.
-struct PendingStores {
-  uint16_t *cdst;
-  int32_t *vdst;
-  uint32_t check;
-  int32_t verdict;
+// ---- per-frame parse / verdict / check (shared by both kernel families) -----
+
+struct Header {
+  int u;              // udp header offset 14 + 4*ihl (ihl unvalidated, :52)
+  bool ipv4, udp;
+  uint32_t pseudo;    // :57-65, read before the check is cleared
+  uint32_t old_check; // f[u+6..u+7], counted as 0 (:68)
 };
 
-__device__ __forceinline__ PendingStores sink_stores() {
-  return PendingStores{reinterpret_cast<uint16_t *>(g_sink), reinterpret_cast<int32_t *>(g_sink + 1), 0u, 0};
+// Frame byte i is at LDS address hb + i (hb may be unaligned).
+__device__ __forceinline__ Header parse_header(uint32_t hb) {
+  Header h;
+  const uint32_t w12 = lds_u32(hb + 12);   // f[12..15]
+  const uint32_t w20 = lds_u32(hb + 20);   // f[20..23]
+  const uint32_t w24 = lds_u32(hb + 24);   // f[24..27]
+  const uint32_t w28 = lds_u32(hb + 28);   // f[28..31]
+  const uint32_t w32 = lds_u32(hb + 32);   // f[32..35]
+  h.u = 14 + 4 * ((w12 >> 16) & 0x0f);
+  const uint32_t wu = lds_u32(hb + h.u + 4);  // f[u+4..u+7]
+  h.ipv4 = (w12 & 0xffffu) == 0x0008u;        // f[12..13] == 08 00
+  h.udp = (w20 >> 24) == 17u;                 // f[23]
+  // le16(26) + le16(28) + le16(30) + le16(32) + 17<<8 + le16(u+4)
+  h.pseudo = (w24 >> 16) + (w28 & 0xffffu) + (w28 >> 16) + (w32 & 0xffffu) + 0x1100u + (wu & 0xffffu);
+  h.old_check = wu >> 16;
+  return h;
 }
 
-__device__ __forceinline__ void issue(const PendingStores &ps, uint32_t defer) {
-  if (!defer) *ps.cdst = static_cast<uint16_t>(ps.check);      // :108
-  *ps.vdst = ps.verdict;
+// checksummer_user.c:34-55 and :110-111
+__device__ __forceinline__ int32_t verdict_of(const FrameRef &r, const Header &h, int32_t fwd, bool &do_sum) {
+  do_sum = false;
+  if (!r.live) return -1;                 // :34-37 (and out-of-range descriptors)
+  if (!h.ipv4) return 0;                  // :39-41
+  if (r.len < 34) return -1;              // :43-46
+  if (!h.udp) return 0;                   // :48-50
+  if (h.u + 8 > r.len) return -1;         // :53-55
+  do_sum = true;
+  return fwd;                             // :110-111
 }
 
+// :92-108 given the reduced payload sum P (old check still included)
+__device__ __forceinline__ uint16_t check_of(const Header &h, uint32_t P, uint32_t mult) {
+  const uint32_t s = h.pseudo + mult * (P - h.old_check);
+  return static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));
+}
+
+// The word this frame leaves in verdicts[f] after the summing pass; the check
+// bytes are written here only in single-pass (fused) mode.
+__device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const FrameRef &r, const Header &h,
+                                                int32_t verdict, bool do_sum, uint32_t P) {
+  if (!do_sum) return verdict;
+  const uint16_t c = check_of(h, P, a.payload_mult);
+  if (a.defer) return static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
+  *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+  return verdict;
+}
+
+// Frames longer than one pass: the remaining passes as direct loads.
 template <int LPF, int NCH>
-__device__ __forceinline__ PendingStores process_frame(const KernelArgs &args, const FrameRef &r,
-                                                       uint32_t f, const uint4 (&v)[NCH],
-                                                       uint8_t *slot, int gl) {
+__device__ __forceinline__ void tail_passes(const FrameRef &r, int gl, int lo, int hi, uint32_t wl,
+                                            uint32_t wh, uint32_t &acc_lo, uint32_t &acc_hi) {
   constexpr int SPAN = LPF * NCH;
-  // Stage window chunks 0..6 in LDS shifted by -rs, so frame byte i sits at
-  // slot[16 + i] whatever the frame's alignment: the header fields are then at
-  // fixed offsets.  One wave's LDS accesses execute in issue order; only the
-  // compiler must be kept from moving the reads above the writes.
+  for (int p = SPAN; p < r.nch; p += SPAN) {
+    uint4 t[NCH];
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int c = k * LPF + gl;
-    if (k * LPF < kHdrChunks && c < kHdrChunks)
-      *reinterpret_cast<uint4 *>(slot + 16 + 16 * c - r.rs) = v[k];
+    for (int k = 0; k < NCH; ++k) t[k] = load_nt(r.cp + min(p + k * LPF + gl, r.nch - 1));
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) chunk_sum(t[k], (p + k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
   }
+}
+
+// Write a finished tile's results (LDS rec[0..63]) as one coalesced store.
+__device__ __forceinline__ void flush_tile(const KernelArgs &a, uint32_t rec, uint32_t tile_f0, int lane) {
   compiler_barrier();
-  const uint4 q0 = *reinterpret_cast<const uint4 *>(slot + 16);   // f[0..15]
-  const uint4 q1 = *reinterpret_cast<const uint4 *>(slot + 32);   // f[16..31]
-  const uint32_t w8 = *reinterpret_cast<const uint32_t *>(slot + 48);  // f[32..35]
-  const int ihl = (q0.w >> 16) & 0x0f;                             // f[14] low nibble
-  const int u = 14 + 4 * ihl;                                      // :52, ihl unvalidated
-  const uint32_t wa = *reinterpret_cast<const uint32_t *>(slot + 16 + u + 2);  // f[u+2..u+5]
-  const uint32_t wb = *reinterpret_cast<const uint32_t *>(slot + 16 + u + 6);  // f[u+6..u+9]
+  const int32_t v = lds_i32(rec + 4 * lane);
+  if (tile_f0 + lane < a.n) a.verdicts[tile_f0 + lane] = v;
   compiler_barrier();
-
-  const bool ipv4 = (q0.w & 0xffffu) == 0x0008u;                  // f[12..13] == 08 00
-  const bool udp = (q1.y >> 24) == 17u;                           // f[23]
-  int32_t verdict;
-  bool do_sum = false;
-  if (!r.live) {
-    verdict = -1;                                   // :34-37 (and out-of-range descriptors)
-  } else if (!ipv4) {
-    verdict = 0;                                    // :39-41
-  } else if (r.len < 34) {
-    verdict = -1;                                   // :43-46
-  } else if (!udp) {
-    verdict = 0;                                    // :48-50
-  } else if (u + 8 > r.len) {
-    verdict = -1;                                   // :53-55
-  } else {
-    verdict = args.fwd_verdict;                     // :110-111
-    do_sum = true;
-  }
-
-  // Pass-0 partial sums on every path (also for frames that end up unsummed):
-  // every loaded register is consumed unconditionally, so no load of this frame
-  // can still be in flight at the loop back-edge.
-  const int lo = r.rs + u;
-  const int hi = r.rs + r.len;
-  const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
-  const uint32_t wh = wl << 8 | wl >> 24;
-  uint32_t acc_lo = 0, acc_hi = 0;
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-
-  uint16_t check = 0;
-  if (do_sum) {
-    // :57-65 pseudo-header, read before the check is cleared:
-    // le16(26) + le16(28) + le16(30) + le16(32) + 17<<8 + le16(u+4)
-    uint32_t s = (q1.z >> 16) + (q1.w & 0xffffu) + (q1.w >> 16) + (w8 & 0xffffu) + 0x1100u + (wa >> 16);
-    const uint32_t old_check = wb & 0xffffu;        // counted as 0 (:68)
-    for (int p = SPAN; p < r.nch; p += SPAN) {      // frames longer than one pass
-      uint4 t[NCH];
-      load_pass<LPF, NCH>(r, p, gl, t);
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) chunk_sum(t[k], (p + k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-    }
-    uint32_t P = group_sum<LPF>(acc_lo + (acc_hi << 8));
-    P -= old_check;
-    s += args.payload_mult * P;                     // :92-103, iterations in closed form
-    check = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));  // :105-106
-  }
-  PendingStores ps;
-  ps.cdst = do_sum ? reinterpret_cast<uint16_t *>(r.fp + u + 6) : reinterpret_cast<uint16_t *>(g_sink);
-  ps.vdst = r.exists ? args.verdicts + f : reinterpret_cast<int32_t *>(g_sink + 1);
-  ps.check = check;
-  ps.verdict = (args.defer && do_sum) ? make_record(u, check) : verdict;
-  compiler_barrier();   // the next frame rewrites this group's LDS slot
-  return ps;
 }
 
-// The G descriptors of one wave's frames are contiguous, so they are fetched
-// with wave-uniform scalar loads (s_load, counted by lgkmcnt): the descriptor
-// prefetch then never forces the compiler to drain the vector-memory counter
-// that the chunk loads of the next frame are still running on.
-typedef const __attribute__((address_space(4))) xsknf_gpu_desc *const_desc_ptr;
-
-template <int G>
-struct DescSet {
-  uint64_t addr[G];
-  uint32_t len[G];
-};
-
-template <int G>
-__device__ __forceinline__ DescSet<G> load_descs(const KernelArgs &a, uint32_t wf, uint32_t last) {
-  DescSet<G> ds;
-  const const_desc_ptr cd = (const_desc_ptr)(reinterpret_cast<uintptr_t>(a.descs));
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const uint32_t i = min(wf + g, last);
-    ds.addr[g] = cd[i].addr;
-    ds.len[g] = cd[i].len;
-  }
-  return ds;
-}
-
-template <int G>
-__device__ __forceinline__ xsknf_gpu_desc pick(const DescSet<G> &ds, int grp) {
-  xsknf_gpu_desc d;
-  d.addr = ds.addr[0];
-  d.len = ds.len[0];
-#pragma unroll
-  for (int g = 1; g < G; ++g) {
-    d.addr = grp == g ? ds.addr[g] : d.addr;
-    d.len = grp == g ? ds.len[g] : d.len;
-  }
-  d.options = 0;
-  return d;
-}
+// ---- register kernel ----------------------------------------------------------
 
 template <int LPF, int NCH, int U>
 __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args) {
-  static_assert(kWave % LPF == 0, "LPF must divide the wave");
+  static_assert(kWave % LPF == 0 && LPF >= 4, "LPF must divide the wave");
   static_assert(LPF * NCH >= kHdrChunks, "pass 0 must cover the header window");
-  constexpr int G = kWave / LPF;     // frame groups per wave
-  constexpr int FW = G * U;          // frames per wave per iteration
-  static_assert(FW <= 8, "descriptor prefetch is held in SGPRs");
+  constexpr int G = kWave / LPF;
+  constexpr int FPS = G * U;                 // frames per wave step
+  constexpr int SPT = kTile / FPS;           // steps per tile
+  static_assert(kTile % FPS == 0, "steps tile the tile");
 
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock][G][kSlotBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t hdr[kWavesPerBlock][G][kSlotBytes];
+  __shared__ __attribute__((aligned(16))) int32_t recs[kWavesPerBlock][kTile];
+  __shared__ __attribute__((aligned(16))) xsknf_gpu_desc dtile[kWavesPerBlock][kTile];
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int grp = lane / LPF;
   const int gl = lane % LPF;
-  uint8_t *slot = &lds[wv][grp][0];
-  const uint32_t wstride = gridDim.x * kWavesPerBlock * FW;   // frames per grid sweep
+  const uint32_t slot = lds_addr(&hdr[wv][grp][0]);
+  const uint32_t rec = lds_addr(&recs[wv][0]);
+  const uint32_t dsc = lds_addr(&dtile[wv][0]);
+  const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t last = args.n - 1;
-  uint32_t wf = (blockIdx.x * kWavesPerBlock + wv) * FW;      // this wave's first frame
 
-  // Each iteration issues the chunk loads of U frames per group at once, then
-  // reduces them one by one (frame u+1's loads stay in flight while frame u is
-  // parsed and summed).  Nothing is carried in flight across the back-edge:
-  // descriptors for the next iteration are prefetched with scalar loads.
-  DescSet<FW> dcur = load_descs<FW>(args, wf, last);
-  while (wf < args.n) {          // wave-uniform loop control
-    FrameRef ref[U];
-    uint4 v[U][NCH];
+  // the next tile's descriptors ride in VGPRs (one per lane) a tile ahead
+  uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
+  uint4 dnext = *reinterpret_cast<const uint4 *>(args.descs + min(tile * kTile + lane, last));
+  for (; tile * kTile < args.n; tile += waves) {
+    const uint32_t tf0 = tile * kTile;
+    compiler_barrier();
+    lds_store_u128(dsc + 16 * lane, dnext);
+    compiler_barrier();
+    dnext = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * kTile + lane, last));
+    for (int st = 0; st < SPT; ++st) {
+      const uint32_t i0 = st * FPS;          // tile-relative index of the step's first frame
+      FrameRef ref[U];
+      uint4 v[U][NCH];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t f = wf + u * G + grp;
-      ref[u] = make_ref(args, pick<FW>(dcur, u * G + grp), f < args.n);
-      load_pass<LPF, NCH>(ref[u], 0, gl, v[u]);
-    }
-    const uint32_t wn = wf + wstride;
-    dcur = load_descs<FW>(args, wn, last);
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * G + grp;
+        ref[u] = ref_from_lds(args, dsc + 16 * i, tf0 + i);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      issue(process_frame<LPF, NCH>(args, ref[u], wf + u * G + grp, v[u], slot, gl), args.defer);
+        for (int k = 0; k < NCH; ++k) v[u][k] = load_nt(ref[u].cp + min(k * LPF + gl, ref[u].nch - 1));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const FrameRef &r = ref[u];
+        // header window (chunks 0..6) to LDS; one wave's LDS accesses execute in
+        // issue order, only the compiler must not move reads above the writes
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+          const int c = k * LPF + gl;
+          if (k * LPF < kHdrChunks && c < kHdrChunks) lds_store_u128(slot + 16 * c, v[u][k]);
+        }
+        compiler_barrier();
+        const Header h = parse_header(slot + r.rs);
+        bool do_sum;
+        const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
+        const int lo = r.rs + h.u, hi = r.rs + r.len;
+        const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+        const uint32_t wh = wl << 8 | wl >> 24;
+        uint32_t acc_lo = 0, acc_hi = 0;
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) chunk_sum(v[u][k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+        if (do_sum) tail_passes<LPF, NCH>(r, gl, lo, hi, wl, wh, acc_lo, acc_hi);
+        const uint32_t P = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
+        if (gl == LPF - 1 && r.exists)
+          lds_store_i32(rec + 4 * (i0 + u * G + grp), frame_result(args, r, h, verdict, do_sum, P));
+        compiler_barrier();   // the next frame rewrites this group's header window
+      }
     }
-    wf = wn;
+    flush_tile(args, rec, tf0, lane);
   }
 }
 
-// ---- LDS-DMA ring variant --------------------------------------------------
+// ---- LDS-DMA ring kernel ------------------------------------------------------
 //
-// Each wave streams its frames through a private ring of R slots in LDS filled
-// by global_load_lds_dwordx4 (LDS-DMA: 16 B per lane straight into LDS, no VGPR
-// destination).  At step i the wave issues the DMA of step i+R-1 and then waits
-// -- with an explicitly counted vmcnt -- only for step i's slot, so R-1 steps of
-// loads stay in flight while step i is parsed, summed and reduced, and the
-// loads cost no registers (occupancy stays high).  The DMA is issued from
+// Each wave streams its steps (G frames, one per group) through a private ring
+// of R LDS slots filled by global_load_lds_dwordx4 (16 B per lane straight into
+// LDS).  At step j the wave issues the DMA of step j+R-1, then waits -- with an
+// explicitly counted vmcnt -- only for step j's slot.  The DMA is issued from
 // inline asm because the compiler drains vmcnt to 0 before every LDS read once
-// it sees an LDS-DMA in flight; the waits here count only this wave's own DMAs
-// that are younger than the slot being read (other vector-memory operations
-// can only make the wait stricter, never too weak).
+// it sees an LDS-DMA in flight; the waits count only this wave's DMAs younger
+// than the slot being read (other vector-memory operations can only make such
+// a wait stricter, never too weak).  Before a slot is refilled, every read of
+// it has been consumed (its data fed the previous step's reduction).
 //
 // Slot layout: DMA instruction k of a step writes 1 KiB at slot + k*1024, lane l
-// at +16*l, so group g's chunk c = k*LPF + gl sits at slot + k*1024 + g*LPF*16 +
-// gl*16, and chunks 0..LPF-1 of a frame (bytes [0, 16*LPF - rs) of the frame,
-// every header byte for LPF >= 8) are contiguous at slot + g*LPF*16.
+// at +16*l: group g's chunk c = k*LPF + gl sits at slot + k*1024 + 16*(g*LPF + gl),
+// and the frame's chunks 0..LPF-1 (every header byte for LPF >= 8) are
+// contiguous at slot + 16*g*LPF.
 
-__device__ __forceinline__ void dma16(const void *gaddr, uint32_t lds_addr) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
-               :: "v"(gaddr), "s"(lds_addr) : "memory", "m0");
+__device__ __forceinline__ void dma16_nt(const void *gaddr, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt"
+               :: "v"(gaddr), "s"(lds) : "memory", "m0");
 }
 
 template <int N>
@@ -372,177 +376,110 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
 }
 
-__device__ __forceinline__ uint32_t lds_u32(uint32_t addr) {
-  // may be unaligned: gfx950 LDS serves unaligned dword reads
-  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(static_cast<uintptr_t>(addr));
-}
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint4 lds_u128(uint32_t addr) {
-  const u32x4 x = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(static_cast<uintptr_t>(addr));
-  return make_uint4(x.x, x.y, x.z, x.w);
-}
-
-// Group sum via DPP: the total lands in the group's LAST lane (lane LPF-1).
-template <int LPF>
-__device__ __forceinline__ uint32_t group_sum_last(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);   // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);   // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);   // row_shr:4
-  if constexpr (LPF >= 16) v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);  // row_shr:8
-  if constexpr (LPF >= 32) v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
-  if constexpr (LPF >= 64) v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
-  return v;
-}
-
-// Issue the NCH DMAs of one frame window per group into `slot` (chunk index
-// clamped into the window, as in load_pass).
-template <int LPF, int NCH>
-__device__ __forceinline__ void dma_pass(const FrameRef &r, int gl, uint32_t slot) {
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int c = min(k * LPF + gl, r.nch - 1);
-    dma16(r.cp + c, slot + k * 1024);
-  }
-}
-
-// Parse + sum + reduce one frame per group from a landed slot; returns the
-// frame's stores (issued by the group's last lane).
-template <int LPF, int NCH>
-__device__ __forceinline__ void process_slot(const KernelArgs &args, const FrameRef &r, uint32_t f,
-                                             uint32_t slot, int grp, int gl, int lane) {
-  constexpr int SPAN = LPF * NCH;
-  const uint32_t hb = slot + grp * LPF * 16 + r.rs;        // frame byte i at hb + i
-  const uint32_t w12 = lds_u32(hb + 12);                   // f[12..15]
-  const uint32_t w20 = lds_u32(hb + 20);                   // f[20..23]
-  const uint32_t w24 = lds_u32(hb + 24);                   // f[24..27]
-  const uint32_t w28 = lds_u32(hb + 28);                   // f[28..31]
-  const uint32_t w32 = lds_u32(hb + 32);                   // f[32..35]
-  const int u = 14 + 4 * ((w12 >> 16) & 0x0f);             // :52, ihl unvalidated
-  const uint32_t wu = lds_u32(hb + u + 4);                 // f[u+4..u+7]: udp len, old check
-  uint4 v[NCH];
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) v[k] = lds_u128(slot + k * 1024 + lane * 16);
-
-  const bool ipv4 = (w12 & 0xffffu) == 0x0008u;           // f[12..13] == 08 00
-  const bool udp = (w20 >> 24) == 17u;                     // f[23]
-  int32_t verdict;
-  bool do_sum = false;
-  if (!r.live) {
-    verdict = -1;                                   // :34-37 (and out-of-range descriptors)
-  } else if (!ipv4) {
-    verdict = 0;                                    // :39-41
-  } else if (r.len < 34) {
-    verdict = -1;                                   // :43-46
-  } else if (!udp) {
-    verdict = 0;                                    // :48-50
-  } else if (u + 8 > r.len) {
-    verdict = -1;                                   // :53-55
-  } else {
-    verdict = args.fwd_verdict;                     // :110-111
-    do_sum = true;
-  }
-
-  const int lo = r.rs + u;
-  const int hi = r.rs + r.len;
-  const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
-  const uint32_t wh = wl << 8 | wl >> 24;
-  uint32_t acc_lo = 0, acc_hi = 0;
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-  if (do_sum) {
-    for (int p = SPAN; p < r.nch; p += SPAN) {      // frames longer than one pass: direct loads
-      uint4 t[NCH];
-      load_pass<LPF, NCH>(r, p, gl, t);
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) chunk_sum(t[k], (p + k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-    }
-  }
-  const uint32_t P = group_sum_last<LPF>(acc_lo + (acc_hi << 8)) - (wu >> 16);   // old check counted as 0 (:68)
-  if (gl == LPF - 1 && r.exists) {
-    if (do_sum) {
-      // :57-65 pseudo-header: le16(26) + le16(28) + le16(30) + le16(32) + 17<<8 + le16(u+4)
-      uint32_t s = (w24 >> 16) + (w28 & 0xffffu) + (w28 >> 16) + (w32 & 0xffffu) + 0x1100u + (wu & 0xffffu);
-      s += args.payload_mult * P;                   // :92-103, iterations in closed form
-      const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));  // :105-106
-      if (args.defer) {
-        verdict = make_record(u, c);
-      } else {
-        *reinterpret_cast<uint16_t *>(r.fp + u + 6) = c;   // :108
-      }
-    }
-    args.verdicts[f] = verdict;
-  }
-}
-
 template <int LPF, int NCH, int R>
 __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs args) {
   static_assert(kWave % LPF == 0 && LPF >= 8, "header window must sit in chunk slot k = 0");
-  static_assert(R >= 2 && R <= 4, "ring depth");
-  static_assert((R - 1) * NCH < 64, "vmcnt range");
+  static_assert(R >= 2 && R <= 4 && (R - 1) * NCH < 64, "ring depth / vmcnt range");
   constexpr int G = kWave / LPF;
   constexpr int SLOT = NCH * 1024;
-  static_assert(G <= 8, "descriptor prefetch is held in SGPRs");
+  constexpr int SPT = kTile / G;             // steps per tile
+  static_assert(SPT >= 2 * R - 1, "a tile's descriptor DMA lands before its first frame DMA");
 
   __shared__ __attribute__((aligned(1024))) uint8_t ring[kWavesPerBlock][R][SLOT];
+  __shared__ __attribute__((aligned(16))) int32_t recs[kWavesPerBlock][kTile];
+  __shared__ __attribute__((aligned(1024))) xsknf_gpu_desc dtile[kWavesPerBlock][2][kTile];
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int grp = lane / LPF;
   const int gl = lane % LPF;
-  const uint32_t ring0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(&ring[wv][0][0]));
-  const uint32_t wstride = gridDim.x * kWavesPerBlock * G;
+  const uint32_t ring0 = lds_addr(&ring[wv][0][0]);
+  const uint32_t rec = lds_addr(&recs[wv][0]);
+  const uint32_t dsc0 = lds_addr(&dtile[wv][0][0]);
+  const uint32_t waves = gridDim.x * kWavesPerBlock;
+  const uint32_t wg = blockIdx.x * kWavesPerBlock + wv;
   const uint32_t last = args.n - 1;
-  const uint32_t w0 = (blockIdx.x * kWavesPerBlock + wv) * G;
 
-  // frames of step j of this wave: w0 + j * wstride + grp
+  // Step j of this wave covers tile k = j / SPT (global tile wg + k*waves),
+  // frames (j % SPT)*G + grp of it.  Tile k's descriptors sit in dtile[k & 1],
+  // DMA'd when tile k-1 starts (tile 0 and 1 in the prologue).
+  auto tile_f0 = [&](uint32_t k) -> uint32_t { return (wg + k * waves) * kTile; };
+  auto dma_descs = [&](uint32_t k) {
+    dma16_nt(args.descs + min(tile_f0(k) + lane, last), dsc0 + (k & 1) * (kTile * 16));
+  };
+  auto ref_of_step = [&](uint32_t j) -> FrameRef {
+    const uint32_t i = (j % SPT) * G + grp;
+    return ref_from_lds(args, dsc0 + ((j / SPT) & 1) * (kTile * 16) + 16 * i, tile_f0(j / SPT) + i);
+  };
+  auto issue = [&](const FrameRef &r, int s) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) dma16_nt(r.cp + min(k * LPF + gl, r.nch - 1), ring0 + s * SLOT + k * 1024);
+  };
+
+  dma_descs(0);
+  dma_descs(1);
+  wait_vmcnt<1>();                      // tile 0's descriptors
   FrameRef ref[R];
-  // prologue: steps 0 .. R-2 in flight
 #pragma unroll
   for (int j = 0; j < R - 1; ++j) {
-    const uint32_t wf = w0 + j * wstride;
-    ref[j] = make_ref(args, pick<G>(load_descs<G>(args, wf, last), grp), wf + grp < args.n);
-    dma_pass<LPF, NCH>(ref[j], gl, ring0 + j * SLOT);
+    ref[j] = ref_of_step(j);
+    issue(ref[j], j);
   }
-  DescSet<G> dpre = load_descs<G>(args, w0 + (R - 1) * wstride, last);
 
-  // Unrolled by R so ring slots and the per-step FrameRefs are static.
-  uint32_t wf = w0;
+  uint32_t j = 0;
   while (true) {
 #pragma unroll
-    for (int s = 0; s < R; ++s) {
-      if (wf >= args.n) {        // wave-uniform exit; drain this wave's DMAs first
-        wait_vmcnt<0>();
+    for (int s = 0; s < R; ++s) {       // unrolled so ring slots and refs are static
+      const uint32_t tk = j / SPT, js = j % SPT;
+      const uint32_t f0 = tile_f0(tk);
+      if (f0 >= args.n) {               // wave-uniform exit (tiles ascend)
+        wait_vmcnt<0>();                // no DMA may land after the workgroup ends
         return;
       }
-      const int sn = (s + R - 1) % R;                  // slot of step i+R-1 (freed by step i-1)
-      const uint32_t wn = wf + (R - 1) * wstride;
-      ref[sn] = make_ref(args, pick<G>(dpre, grp), wn + grp < args.n);
-      dpre = load_descs<G>(args, wn + wstride, last);
-      dma_pass<LPF, NCH>(ref[sn], gl, ring0 + sn * SLOT);
-      wait_vmcnt<(R - 1) * NCH>();                     // step i's slot has landed
-      process_slot<LPF, NCH>(args, ref[s], wf + grp, ring0 + s * SLOT, grp, gl, lane);
-      wf += wstride;
+      if (js == 0 && tk > 0) dma_descs(tk + 1);   // tile k+1 behind tile k-1's last reads
+      const int sn = (s + R - 1) % R;   // slot of step j+R-1, freed by step j-1
+      ref[sn] = ref_of_step(j + R - 1);
+      issue(ref[sn], sn);
+      wait_vmcnt<(R - 1) * NCH>();      // step j's slot (and older DMAs) have landed
+
+      const FrameRef &r = ref[s];
+      const uint32_t sl = ring0 + s * SLOT;
+      const Header h = parse_header(sl + 16 * grp * LPF + r.rs);
+      uint4 v[NCH];
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) v[k] = lds_u128(sl + k * 1024 + 16 * lane);
+      bool do_sum;
+      const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
+      const int lo = r.rs + h.u, hi = r.rs + r.len;
+      const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+      const uint32_t wh = wl << 8 | wl >> 24;
+      uint32_t acc_lo = 0, acc_hi = 0;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+      if (do_sum) tail_passes<LPF, NCH>(r, gl, lo, hi, wl, wh, acc_lo, acc_hi);
+      const uint32_t P = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
+      if (gl == LPF - 1 && r.exists)
+        lds_store_i32(rec + 4 * (js * G + grp), frame_result(args, r, h, verdict, do_sum, P));
+      if (js == SPT - 1) flush_tile(args, rec, f0, lane);   // steps past n ran as no-ops
+      ++j;
     }
   }
 }
 
-// Phase 2 of the two-phase stores: write the parked check bytes into the
-// frames (checksummer_user.c:108) and the final verdicts (:110-111).
+// ---- phase 2: write-only scatter of the parked checks (:108) and verdicts ----
+
 __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) {
   for (uint32_t f = blockIdx.x * kBlock + threadIdx.x; f < args.n; f += gridDim.x * kBlock) {
-    const uint32_t rec = static_cast<uint32_t>(args.verdicts[f]);
-    if ((rec & kRecTagMask) == kRecTag) {
+    const uint32_t r = static_cast<uint32_t>(args.verdicts[f]);
+    if ((r & kRecTagMask) == kRecTag) {
       const uint64_t off = umem_offset(args.descs[f].addr);
-      const uint32_t u = (rec >> 16) & 0x7f;
-      *reinterpret_cast<uint16_t *>(args.umem + off + u + 6) = static_cast<uint16_t>(rec & 0xffffu);
+      *reinterpret_cast<uint16_t *>(args.umem + off + ((r >> 16) & 0x7f) + 6) = static_cast<uint16_t>(r);
       args.verdicts[f] = args.fwd_verdict;
     }
   }
 }
 
-// ---- host side -------------------------------------------------------------
+// ---- host side ----------------------------------------------------------------
 
 thread_local char g_last_error[256] = "";
 
@@ -550,81 +487,67 @@ void set_error(hipError_t e, const char *where) {
   snprintf(g_last_error, sizeof(g_last_error), "%s: %s", where, hipGetErrorString(e));
 }
 
-struct DeviceInfo {
-  int cus = 0;
-  bool ok = false;
-};
-
-DeviceInfo device_info(int dev) {
-  static DeviceInfo cache[64];
-  if (dev < 0 || dev >= 64) return DeviceInfo{};
-  if (!cache[dev].ok) {
+int device_cus() {
+  static int cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
     int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
-      cache[dev].cus = cus;
-      cache[dev].ok = true;
-    }
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return 256;
+    cache[dev] = cus;
   }
   return cache[dev];
 }
 
-hipError_t launch_scatter(const KernelArgs &a, hipStream_t stream, const DeviceInfo &di) {
-  const uint32_t cap = static_cast<uint32_t>((di.ok ? di.cus : 256) * 8);
-  const uint32_t need = (a.n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
-  return hipGetLastError();
+// persistent grid: enough blocks for every tile, at most blocks_per_cu per CU
+uint32_t grid_blocks(uint32_t n, int blocks_per_cu) {
+  const uint32_t tiles = (n + kTile - 1) / kTile;
+  const uint32_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint32_t cap = static_cast<uint32_t>(device_cus() * blocks_per_cu);
+  return need < cap ? need : cap;
+}
+
+int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && a.defer) {
+    const uint32_t need = (a.n + kBlock - 1) / kBlock;
+    const uint32_t cap = static_cast<uint32_t>(device_cus() * 8);
+    hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
+    e = hipGetLastError();
+    what = "scatter_checks launch";
+  }
+  if (e != hipSuccess) { set_error(e, what); return -EIO; }
+  return 0;
 }
 
 template <int LPF, int NCH, int U>
-int launch(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  constexpr int G = kWave / LPF;
-  constexpr int frames_per_block = kWavesPerBlock * G * U;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) { set_error(e, "hipGetDevice"); return -EIO; }
-  const DeviceInfo di = device_info(dev);
-  const uint32_t cap = static_cast<uint32_t>((di.ok ? di.cus : 256) * blocks_per_cu);
-  const uint32_t need = (a.n + frames_per_block - 1) / frames_per_block;
-  const uint32_t blocks = need < cap ? need : cap;
-  hipLaunchKernelGGL((checksum_kernel<LPF, NCH, U>), dim3(blocks), dim3(kBlock), 0, stream, a);
-  e = hipGetLastError();
-  if (e == hipSuccess && a.defer) e = launch_scatter(a, stream, di);
-  if (e != hipSuccess) { set_error(e, "checksum_kernel launch"); return -EIO; }
-  return 0;
+int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
+  hipLaunchKernelGGL((checksum_kernel<LPF, NCH, U>), dim3(grid_blocks(a.n, blocks_per_cu)), dim3(kBlock), 0,
+                     stream, a);
+  return finish_launch(a, stream, "checksum_kernel launch");
 }
 
 template <int LPF, int NCH, int R>
 int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  constexpr int G = kWave / LPF;
-  constexpr int frames_per_block = kWavesPerBlock * G;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) { set_error(e, "hipGetDevice"); return -EIO; }
-  const DeviceInfo di = device_info(dev);
-  const uint32_t cap = static_cast<uint32_t>((di.ok ? di.cus : 256) * blocks_per_cu);
-  const uint32_t need = (a.n + frames_per_block - 1) / frames_per_block;
-  const uint32_t blocks = need < cap ? need : cap;
-  hipLaunchKernelGGL((checksum_kernel_dma<LPF, NCH, R>), dim3(blocks), dim3(kBlock), 0, stream, a);
-  e = hipGetLastError();
-  if (e == hipSuccess && a.defer) e = launch_scatter(a, stream, di);
-  if (e != hipSuccess) { set_error(e, "checksum_kernel_dma launch"); return -EIO; }
-  return 0;
+  hipLaunchKernelGGL((checksum_kernel_dma<LPF, NCH, R>), dim3(grid_blocks(a.n, blocks_per_cu)), dim3(kBlock),
+                     0, stream, a);
+  return finish_launch(a, stream, "checksum_kernel_dma launch");
 }
 
 // Instantiated launch shapes: {lanes per frame, 16-B chunks per lane and pass,
-// frames per group and iteration}.  The default picks one by frame_len_hint.
+// frames per group and step (register), LDS ring slots (0 = register kernel)}.
 struct Variant {
   int lpf, nch, u, ring;
   int (*fn)(const KernelArgs &, hipStream_t, int);
 };
 
-#define XSKNF_V(L, N, U) {L, N, U, 0, &launch<L, N, U>}
+#define XSKNF_V(L, N, U) {L, N, U, 0, &launch_reg<L, N, U>}
 #define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
 const Variant kVariants[] = {
-    XSKNF_V(8, 1, 1),  XSKNF_V(16, 1, 1), XSKNF_V(16, 1, 2), XSKNF_V(16, 2, 1), XSKNF_V(16, 2, 2),
-    XSKNF_V(32, 1, 1), XSKNF_V(32, 1, 2), XSKNF_V(32, 2, 1), XSKNF_V(32, 2, 2), XSKNF_V(32, 3, 1),
-    XSKNF_V(32, 3, 2), XSKNF_V(64, 1, 1), XSKNF_V(64, 2, 1), XSKNF_V(64, 2, 2), XSKNF_V(64, 3, 1),
-    XSKNF_V(64, 4, 1), XSKNF_V(64, 4, 2), XSKNF_V(64, 6, 1), XSKNF_V(64, 9, 1),
+    XSKNF_V(8, 1, 1),  XSKNF_V(16, 1, 2), XSKNF_V(16, 2, 1), XSKNF_V(16, 2, 2), XSKNF_V(32, 2, 1),
+    XSKNF_V(32, 2, 2), XSKNF_V(32, 3, 1), XSKNF_V(32, 3, 2), XSKNF_V(64, 2, 1), XSKNF_V(64, 4, 1),
+    XSKNF_V(64, 9, 1),
     XSKNF_D(8, 1, 3),  XSKNF_D(8, 1, 4),  XSKNF_D(16, 1, 3), XSKNF_D(16, 2, 3), XSKNF_D(32, 2, 3),
     XSKNF_D(32, 3, 2), XSKNF_D(32, 3, 3), XSKNF_D(64, 2, 3), XSKNF_D(64, 2, 4), XSKNF_D(64, 3, 3),
     XSKNF_D(64, 4, 2), XSKNF_D(64, 4, 3),
@@ -638,13 +561,18 @@ const Variant *find_variant(int lpf, int nch, int u, int ring) {
   return nullptr;
 }
 
-// default shape for a length hint: one pass covers hint + 15 bytes of misalignment
-void default_shape(uint32_t hint, int &lpf, int &nch, int &u) {
-  if (hint + 15 <= 128) { lpf = 8; nch = 1; u = 1; }
-  else if (hint + 15 <= 512) { lpf = 16; nch = 2; u = 2; }
-  else if (hint + 15 <= 1536) { lpf = 32; nch = 3; u = 2; }
-  else if (hint + 15 <= 4096) { lpf = 64; nch = 4; u = 2; }
-  else { lpf = 64; nch = 9; u = 1; }
+// Default shape for a length hint: one pass covers hint + 15 bytes of 16-byte
+// misalignment (measured best per size class, tools/tune.py).
+void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
+  c.frames_per_group = 1;
+  c.blocks_per_cu = 8;
+  c.fused_stores = 0;
+  c.lds_ring = 0;
+  if (hint + 15 <= 128) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; }
+  else if (hint + 15 <= 512) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 2; }
+  else if (hint + 15 <= 1536) { c.lanes_per_frame = 32; c.chunks_per_lane = 3; c.frames_per_group = 2; }
+  else if (hint + 15 <= 4096) { c.lanes_per_frame = 64; c.chunks_per_lane = 4; }
+  else { c.lanes_per_frame = 64; c.chunks_per_lane = 9; }
 }
 
 int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_desc *descs, uint32_t n,
@@ -660,13 +588,23 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
   a.verdicts = verdicts;
   a.n = n;
   a.payload_mult = opts->csum_iterations > 0 ? static_cast<uint32_t>(opts->csum_iterations) : 0u;
-  // aligned-down descriptor address: inside the descriptor array's own page
-  a.dummy = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(descs) & ~static_cast<uintptr_t>(15));
   a.fwd_verdict = opts->action == XSKNF_CSUM_ACTION_REDIRECT
                       ? static_cast<int32_t>((ingress_ifindex + 1u) % opts->num_interfaces)
                       : -1;
   a.defer = 1;
+  // aligned-down descriptor address: inside the descriptor array's own page
+  a.dummy = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(descs) & ~static_cast<uintptr_t>(15));
   return 0;
+}
+
+int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
+  if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
+  if (cfg.fused_stores != 0 && cfg.fused_stores != 1) return -EINVAL;
+  const Variant *v = find_variant(cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group, cfg.lds_ring);
+  if (!v) return -EINVAL;
+  KernelArgs a = base;
+  a.defer = cfg.fused_stores ? 0u : 1u;
+  return v->fn(a, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
 }
 
 }  // namespace xsknf_gpu
@@ -687,41 +625,27 @@ const char *xsknf_gpu_last_error(void) { return xsknf_gpu::g_last_error; }
 int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
                              uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
                              int32_t *verdicts, uint32_t frame_len_hint, void *stream) {
-  using namespace xsknf_gpu;
-  KernelArgs a;
-  const int rc = prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
+  xsknf_gpu::KernelArgs a;
+  const int rc = xsknf_gpu::prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
   if (rc != 0) return rc < 0 ? rc : 0;
-  int lpf, nch, u;
-  default_shape(frame_len_hint ? frame_len_hint : 2048u, lpf, nch, u);
-  return find_variant(lpf, nch, u, 0)->fn(a, static_cast<hipStream_t>(stream), 8);
+  xsknf_gpu_launch_cfg cfg;
+  xsknf_gpu::default_cfg(frame_len_hint ? frame_len_hint : 2048u, cfg);
+  return xsknf_gpu::run(a, cfg, stream);
 }
 
 int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
                                  uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
                                  int32_t *verdicts, const struct xsknf_gpu_launch_cfg *cfg, void *stream) {
-  using namespace xsknf_gpu;
-  if (!cfg || cfg->blocks_per_cu < 0 || cfg->blocks_per_cu > 64) return -EINVAL;
-  const Variant *v = find_variant(cfg->lanes_per_frame, cfg->chunks_per_lane, cfg->frames_per_group,
-                                  cfg->lds_ring);
-  if (!v) return -EINVAL;
-  if (cfg->fused_stores != 0 && cfg->fused_stores != 1) return -EINVAL;
-  KernelArgs a;
-  const int rc = prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
+  if (!cfg) return -EINVAL;
+  xsknf_gpu::KernelArgs a;
+  const int rc = xsknf_gpu::prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
   if (rc != 0) return rc < 0 ? rc : 0;
-  a.defer = cfg->fused_stores ? 0u : 1u;
-  return v->fn(a, static_cast<hipStream_t>(stream), cfg->blocks_per_cu ? cfg->blocks_per_cu : 8);
+  return xsknf_gpu::run(a, *cfg, stream);
 }
 
 int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg) {
   if (!cfg) return -EINVAL;
-  int lpf, nch, u;
-  xsknf_gpu::default_shape(frame_len_hint ? frame_len_hint : 2048u, lpf, nch, u);
-  cfg->lanes_per_frame = lpf;
-  cfg->chunks_per_lane = nch;
-  cfg->frames_per_group = u;
-  cfg->blocks_per_cu = 8;
-  cfg->lds_ring = 0;
-  cfg->fused_stores = 0;
+  xsknf_gpu::default_cfg(frame_len_hint ? frame_len_hint : 2048u, *cfg);
   return 0;
 }
 
