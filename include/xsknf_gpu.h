@@ -85,8 +85,10 @@ int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
 /*
  * Launch shape of the batch kernel (tuning / benchmarking).  A group of
  * `lanes_per_frame` lanes (8, 16, 32 or 64) owns one frame at a time and loads
- * `chunks_per_lane` 16-byte chunks per pass; `frames_per_group` frames have
- * their loads in flight together; the persistent grid has `blocks_per_cu`
+ * `chunks_per_lane` 16-byte chunks per pass; in the register kernel a wave
+ * takes tiles of `frames_per_group` consecutive frames per group (the next
+ * frame's loads in flight while the current one is reduced); the persistent
+ * grid has `blocks_per_cu`
  * 256-thread blocks per CU (0 = 8).  `lds_ring` > 0 selects the LDS-DMA
  * kernel, which streams each wave's frames through a ring of that many LDS
  * slots (frames_per_group is then ignored); 0 selects the register kernel.

@@ -98,6 +98,34 @@ __global__ __launch_bounds__(256) void probe_mode(const uint8_t *__restrict__ ba
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// tiled read: wave w owns chunks [64*t, 64*t+64) of tile t = w + k*waves and
+// streams them in order (16-B pieces, 4 loads in flight per lane, nt)
+__global__ __launch_bounds__(256) void probe_tiled(const uint8_t *__restrict__ base, uint64_t chunks,
+                                                   uint32_t ppc, uint32_t stride, uint32_t off,
+                                                   uint32_t *__restrict__ out, uint32_t tile) {
+  uint32_t acc = 0;
+  const uint64_t waves = gridDim.x * 4ull;
+  const uint64_t w = blockIdx.x * 4ull + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  for (uint64_t t = w; t * tile < chunks; t += waves) {
+    const uint64_t pieces = (uint64_t)tile * ppc;
+    for (uint64_t i = lane; i < pieces; i += 256) {
+      uint4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t j = min(i + 64 * k, pieces - 1);
+        const uint64_t c = min(t * tile + j / ppc, chunks - 1), p = j % ppc;
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        const u4v x = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(base + c * stride + off + p * 16));
+        v[k] = make_uint4(x.x, x.y, x.z, x.w);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 // write-only pass: every chunk gets 2 bytes at byte off+40 from a compact u32 array
 __global__ __launch_bounds__(256) void scatter(uint8_t *__restrict__ base, uint64_t chunks,
                                                uint32_t stride, uint32_t off,
@@ -152,6 +180,21 @@ int main(int argc, char **argv) {
       const double us2 = ms2 * 1e3 / reps;
       printf("{\"mode\": \"%s\", \"len\": %u, \"us\": %.2f, \"read_GBps\": %.1f}\n",
              m == 1 ? "reg_nt" : (m == 2 ? "ldsdma" : "ldsdma_nt"), len, us2, rd / us2 / 1e3);
+    }
+  }
+  if (getenv("PROBE_TILED")) {
+    const uint32_t tiles[] = {1, 2, 4, 8, 16, 64};
+    for (uint32_t tl : tiles) {
+      CHECK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL(probe_tiled, dim3(grid), dim3(256), 0, 0, buf, chunks, ppc, stride, off, out, tl);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms2 = 0;
+      CHECK(hipEventElapsedTime(&ms2, e0, e1));
+      const double us2 = ms2 * 1e3 / reps;
+      printf("{\"mode\": \"tiled\", \"tile\": %u, \"len\": %u, \"us\": %.2f, \"read_GBps\": %.1f}\n",
+             tl, len, us2, rd / us2 / 1e3);
     }
   }
   if (getenv("PROBE_SCATTER")) {

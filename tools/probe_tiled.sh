@@ -1,0 +1,8 @@
+#!/bin/bash
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+P=$R/tools/build/hbm_probe
+M=1048576
+export PROBE_TILED=1 PROBE_MODES=1
+timeout -k 10 120 "$P" $M 2048 256 1504 10 0 0
+timeout -k 10 120 "$P" $M 2048 256 64 10 0 0

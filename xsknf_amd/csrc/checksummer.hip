@@ -273,19 +273,56 @@ __device__ __forceinline__ void flush_tile(const KernelArgs &a, uint32_t rec, ui
 }
 
 // ---- register kernel ----------------------------------------------------------
+//
+// A wave works through tiles of SPT steps x G frames (consecutive frames; the
+// grid strides over tiles).  Inside a tile the step loop is fully unrolled over
+// two register buffers: the loads of step s+1 are issued before step s is
+// parsed / summed / reduced, and because the code is straight-line the compiler
+// counts vmcnt exactly (a loop-carried load would make it drain to 0).
 
-template <int LPF, int NCH, int U>
+template <int LPF, int NCH>
+__device__ __forceinline__ void load_frame(const FrameRef &r, int gl, uint4 (&v)[NCH]) {
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) v[k] = load_nt(r.cp + min(k * LPF + gl, r.nch - 1));
+}
+
+template <int LPF, int NCH>
+__device__ __forceinline__ int32_t process_regs(const KernelArgs &args, const FrameRef &r, const uint4 (&v)[NCH],
+                                                uint32_t slot, int gl, uint32_t &P) {
+  // header window (chunks 0..6) to LDS; one wave's LDS accesses execute in issue
+  // order, only the compiler must not move the reads above the writes
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = k * LPF + gl;
+    if (k * LPF < kHdrChunks && c < kHdrChunks) lds_store_u128(slot + 16 * c, v[k]);
+  }
+  compiler_barrier();
+  const Header h = parse_header(slot + r.rs);
+  compiler_barrier();
+  bool do_sum;
+  const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
+  const int lo = r.rs + h.u, hi = r.rs + r.len;
+  const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+  const uint32_t wh = wl << 8 | wl >> 24;
+  uint32_t acc_lo = 0, acc_hi = 0;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+  if (do_sum) tail_passes<LPF, NCH>(r, gl, lo, hi, wl, wh, acc_lo, acc_hi);
+  P = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
+  return (gl == LPF - 1 && r.exists) ? frame_result(args, r, h, verdict, do_sum, P) : 0;
+}
+
+template <int LPF, int NCH, int SPT>
 __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args) {
   static_assert(kWave % LPF == 0 && LPF >= 4, "LPF must divide the wave");
   static_assert(LPF * NCH >= kHdrChunks, "pass 0 must cover the header window");
   constexpr int G = kWave / LPF;
-  constexpr int FPS = G * U;                 // frames per wave step
-  constexpr int SPT = kTile / FPS;           // steps per tile
-  static_assert(kTile % FPS == 0, "steps tile the tile");
+  constexpr int T = SPT * G;                 // frames per tile
+  static_assert(T <= kWave, "one descriptor / result per lane");
 
   __shared__ __attribute__((aligned(16))) uint8_t hdr[kWavesPerBlock][G][kSlotBytes];
-  __shared__ __attribute__((aligned(16))) int32_t recs[kWavesPerBlock][kTile];
-  __shared__ __attribute__((aligned(16))) xsknf_gpu_desc dtile[kWavesPerBlock][kTile];
+  __shared__ __attribute__((aligned(16))) int32_t recs[kWavesPerBlock][kWave];
+  __shared__ __attribute__((aligned(16))) xsknf_gpu_desc dtile[kWavesPerBlock][kWave];
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -297,54 +334,39 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t last = args.n - 1;
 
-  // the next tile's descriptors ride in VGPRs (one per lane) a tile ahead
+  // the next tile's descriptors ride in VGPRs (lane l: frame l of the tile)
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
-  uint4 dnext = *reinterpret_cast<const uint4 *>(args.descs + min(tile * kTile + lane, last));
-  for (; tile * kTile < args.n; tile += waves) {
-    const uint32_t tf0 = tile * kTile;
+  uint4 dnext = *reinterpret_cast<const uint4 *>(args.descs + min(tile * T + min(lane, T - 1), last));
+  for (; tile * T < args.n; tile += waves) {
+    const uint32_t tf0 = tile * T;
     compiler_barrier();
-    lds_store_u128(dsc + 16 * lane, dnext);
+    if (lane < T) lds_store_u128(dsc + 16 * lane, dnext);
     compiler_barrier();
-    dnext = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * kTile + lane, last));
+    dnext = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * T + min(lane, T - 1), last));
+
+    uint4 va[NCH], vb[NCH];
+    FrameRef ra = ref_from_lds(args, dsc + 16 * grp, tf0 + grp), rb;
+    load_frame<LPF, NCH>(ra, gl, va);
+#pragma unroll
     for (int st = 0; st < SPT; ++st) {
-      const uint32_t i0 = st * FPS;          // tile-relative index of the step's first frame
-      FrameRef ref[U];
-      uint4 v[U][NCH];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t i = i0 + u * G + grp;
-        ref[u] = ref_from_lds(args, dsc + 16 * i, tf0 + i);
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) v[u][k] = load_nt(ref[u].cp + min(k * LPF + gl, ref[u].nch - 1));
+      // even steps: process (ra, va), prefetch into (rb, vb); odd steps: swapped
+      FrameRef &rc = (st & 1) ? rb : ra;
+      FrameRef &rn = (st & 1) ? ra : rb;
+      uint4 (&vc)[NCH] = (st & 1) ? vb : va;
+      uint4 (&vn)[NCH] = (st & 1) ? va : vb;
+      if (st + 1 < SPT) {
+        const uint32_t i = (st + 1) * G + grp;
+        rn = ref_from_lds(args, dsc + 16 * i, tf0 + i);
+        load_frame<LPF, NCH>(rn, gl, vn);
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const FrameRef &r = ref[u];
-        // header window (chunks 0..6) to LDS; one wave's LDS accesses execute in
-        // issue order, only the compiler must not move reads above the writes
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) {
-          const int c = k * LPF + gl;
-          if (k * LPF < kHdrChunks && c < kHdrChunks) lds_store_u128(slot + 16 * c, v[u][k]);
-        }
-        compiler_barrier();
-        const Header h = parse_header(slot + r.rs);
-        bool do_sum;
-        const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
-        const int lo = r.rs + h.u, hi = r.rs + r.len;
-        const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
-        const uint32_t wh = wl << 8 | wl >> 24;
-        uint32_t acc_lo = 0, acc_hi = 0;
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) chunk_sum(v[u][k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-        if (do_sum) tail_passes<LPF, NCH>(r, gl, lo, hi, wl, wh, acc_lo, acc_hi);
-        const uint32_t P = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
-        if (gl == LPF - 1 && r.exists)
-          lds_store_i32(rec + 4 * (i0 + u * G + grp), frame_result(args, r, h, verdict, do_sum, P));
-        compiler_barrier();   // the next frame rewrites this group's header window
-      }
+      uint32_t P;
+      const int32_t res = process_regs<LPF, NCH>(args, rc, vc, slot, gl, P);
+      if (gl == LPF - 1 && rc.exists) lds_store_i32(rec + 4 * (st * G + grp), res);
+      compiler_barrier();   // the next frame rewrites this group's header window
     }
-    flush_tile(args, rec, tf0, lane);
+    compiler_barrier();
+    if (lane < T && tf0 + lane < args.n) args.verdicts[tf0 + lane] = lds_i32(rec + 4 * lane);
+    compiler_barrier();
   }
 }
 
@@ -501,8 +523,8 @@ int device_cus() {
 }
 
 // persistent grid: enough blocks for every tile, at most blocks_per_cu per CU
-uint32_t grid_blocks(uint32_t n, int blocks_per_cu) {
-  const uint32_t tiles = (n + kTile - 1) / kTile;
+uint32_t grid_blocks(uint32_t n, int blocks_per_cu, uint32_t tile_frames = kTile) {
+  const uint32_t tiles = (n + tile_frames - 1) / tile_frames;
   const uint32_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
   const uint32_t cap = static_cast<uint32_t>(device_cus() * blocks_per_cu);
   return need < cap ? need : cap;
@@ -521,10 +543,10 @@ int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   return 0;
 }
 
-template <int LPF, int NCH, int U>
+template <int LPF, int NCH, int SPT>
 int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  hipLaunchKernelGGL((checksum_kernel<LPF, NCH, U>), dim3(grid_blocks(a.n, blocks_per_cu)), dim3(kBlock), 0,
-                     stream, a);
+  hipLaunchKernelGGL((checksum_kernel<LPF, NCH, SPT>), dim3(grid_blocks(a.n, blocks_per_cu, SPT * (kWave / LPF))),
+                     dim3(kBlock), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel launch");
 }
 
@@ -542,12 +564,12 @@ struct Variant {
   int (*fn)(const KernelArgs &, hipStream_t, int);
 };
 
-#define XSKNF_V(L, N, U) {L, N, U, 0, &launch_reg<L, N, U>}
+#define XSKNF_V(L, N, S) {L, N, S, 0, &launch_reg<L, N, S>}
 #define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
 const Variant kVariants[] = {
-    XSKNF_V(8, 1, 1),  XSKNF_V(16, 1, 2), XSKNF_V(16, 2, 1), XSKNF_V(16, 2, 2), XSKNF_V(32, 2, 1),
-    XSKNF_V(32, 2, 2), XSKNF_V(32, 3, 1), XSKNF_V(32, 3, 2), XSKNF_V(64, 2, 1), XSKNF_V(64, 4, 1),
-    XSKNF_V(64, 9, 1),
+    XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
+    XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 2), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
+    XSKNF_V(64, 2, 4), XSKNF_V(64, 2, 8), XSKNF_V(64, 4, 4), XSKNF_V(64, 9, 2), XSKNF_V(64, 9, 4),
     XSKNF_D(8, 1, 3),  XSKNF_D(8, 1, 4),  XSKNF_D(16, 1, 3), XSKNF_D(16, 2, 3), XSKNF_D(32, 2, 3),
     XSKNF_D(32, 3, 2), XSKNF_D(32, 3, 3), XSKNF_D(64, 2, 3), XSKNF_D(64, 2, 4), XSKNF_D(64, 3, 3),
     XSKNF_D(64, 4, 2), XSKNF_D(64, 4, 3),
@@ -568,11 +590,11 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.blocks_per_cu = 8;
   c.fused_stores = 0;
   c.lds_ring = 0;
-  if (hint + 15 <= 128) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; }
-  else if (hint + 15 <= 512) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 2; }
-  else if (hint + 15 <= 1536) { c.lanes_per_frame = 32; c.chunks_per_lane = 3; c.frames_per_group = 2; }
-  else if (hint + 15 <= 4096) { c.lanes_per_frame = 64; c.chunks_per_lane = 4; }
-  else { c.lanes_per_frame = 64; c.chunks_per_lane = 9; }
+  if (hint + 15 <= 128) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.frames_per_group = 4; }
+  else if (hint + 15 <= 512) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 4; }
+  else if (hint + 15 <= 1536) { c.lanes_per_frame = 32; c.chunks_per_lane = 3; c.frames_per_group = 4; }
+  else if (hint + 15 <= 4096) { c.lanes_per_frame = 64; c.chunks_per_lane = 4; c.frames_per_group = 4; }
+  else { c.lanes_per_frame = 64; c.chunks_per_lane = 9; c.frames_per_group = 4; }
 }
 
 int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_desc *descs, uint32_t n,
