@@ -121,6 +121,29 @@ __device__ __forceinline__ void chunk_sum(const uint4 v, int x, int lo, int hi, 
   }
 }
 
+// chunk_sum with a wave-uniform fast path: a chunk entirely inside or outside
+// [lo, hi) needs no byte mask, only an include predicate on the weights.  Only
+// when some lane of the wave holds a frame's head or tail chunk (at most two
+// chunk slots per frame) does the wave run the per-byte masks.
+__device__ __forceinline__ void chunk_sum_fast(const uint4 v, int x, int lo, int hi, uint32_t wl,
+                                               uint32_t wh, uint32_t &acc_lo, uint32_t &acc_hi) {
+  const bool inside = x >= lo && x + 16 <= hi;
+  const bool outside = x + 16 <= lo || x >= hi;
+  if (__builtin_amdgcn_ballot_w64(!inside && !outside)) {
+    chunk_sum(v, x, lo, hi, wl, wh, acc_lo, acc_hi);
+  } else {
+    const uint32_t l = inside ? wl : 0u, h = inside ? wh : 0u;
+    acc_lo = __builtin_amdgcn_udot4(v.x, l, acc_lo, false);
+    acc_hi = __builtin_amdgcn_udot4(v.x, h, acc_hi, false);
+    acc_lo = __builtin_amdgcn_udot4(v.y, l, acc_lo, false);
+    acc_hi = __builtin_amdgcn_udot4(v.y, h, acc_hi, false);
+    acc_lo = __builtin_amdgcn_udot4(v.z, l, acc_lo, false);
+    acc_hi = __builtin_amdgcn_udot4(v.z, h, acc_hi, false);
+    acc_lo = __builtin_amdgcn_udot4(v.w, l, acc_lo, false);
+    acc_hi = __builtin_amdgcn_udot4(v.w, h, acc_hi, false);
+  }
+}
+
 // Group sum via DPP (all lanes active): the total lands in the group's LAST lane.
 template <int LPF>
 __device__ __forceinline__ uint32_t group_sum_last(uint32_t v) {
@@ -306,7 +329,7 @@ __device__ __forceinline__ int32_t process_regs(const KernelArgs &args, const Fr
   const uint32_t wh = wl << 8 | wl >> 24;
   uint32_t acc_lo = 0, acc_hi = 0;
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+  for (int k = 0; k < NCH; ++k) chunk_sum_fast(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
   if (do_sum) tail_passes<LPF, NCH>(r, gl, lo, hi, wl, wh, acc_lo, acc_hi);
   P = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
   return (gl == LPF - 1 && r.exists) ? frame_result(args, r, h, verdict, do_sum, P) : 0;
@@ -477,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
       const uint32_t wh = wl << 8 | wl >> 24;
       uint32_t acc_lo = 0, acc_hi = 0;
 #pragma unroll
-      for (int k = 0; k < NCH; ++k) chunk_sum(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+      for (int k = 0; k < NCH; ++k) chunk_sum_fast(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
       if (do_sum) tail_passes<LPF, NCH>(r, gl, lo, hi, wl, wh, acc_lo, acc_hi);
       const uint32_t P = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
       if (gl == LPF - 1 && r.exists)
