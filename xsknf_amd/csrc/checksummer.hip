@@ -545,11 +545,31 @@ int device_cus() {
   return cache[dev];
 }
 
-// persistent grid: enough blocks for every tile, at most blocks_per_cu per CU
-uint32_t grid_blocks(uint32_t n, int blocks_per_cu, uint32_t tile_frames = kTile) {
+// Persistent grid: enough blocks for every tile, but never more than are
+// resident at once (occupancy by VGPR / LDS of the instantiation), capped by
+// blocks_per_cu.  A grid larger than residency would run in rounds with an
+// idle tail, since tiles are dealt to waves statically.
+int resident_blocks(const void *kernel) {
+  struct Entry { const void *k; int dev; int blocks; };
+  static thread_local Entry cache[64];
+  static thread_local int used = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  for (int i = 0; i < used; ++i)
+    if (cache[i].k == kernel && cache[i].dev == dev) return cache[i].blocks;
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kBlock, 0) != hipSuccess || b <= 0) b = 1;
+  if (used < 64) cache[used++] = Entry{kernel, dev, b};
+  return b;
+}
+
+template <typename K>
+uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_frames) {
+  const int resident = resident_blocks(reinterpret_cast<const void *>(kernel));
+  const int per_cu = blocks_per_cu < resident ? blocks_per_cu : resident;
   const uint32_t tiles = (n + tile_frames - 1) / tile_frames;
   const uint32_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  const uint32_t cap = static_cast<uint32_t>(device_cus() * blocks_per_cu);
+  const uint32_t cap = static_cast<uint32_t>(device_cus() * per_cu);
   return need < cap ? need : cap;
 }
 
@@ -568,15 +588,15 @@ int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
 
 template <int LPF, int NCH, int SPT>
 int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  hipLaunchKernelGGL((checksum_kernel<LPF, NCH, SPT>), dim3(grid_blocks(a.n, blocks_per_cu, SPT * (kWave / LPF))),
-                     dim3(kBlock), 0, stream, a);
+  auto k = checksum_kernel<LPF, NCH, SPT>;
+  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, SPT * (kWave / LPF))), dim3(kBlock), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel launch");
 }
 
 template <int LPF, int NCH, int R>
 int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  hipLaunchKernelGGL((checksum_kernel_dma<LPF, NCH, R>), dim3(grid_blocks(a.n, blocks_per_cu)), dim3(kBlock),
-                     0, stream, a);
+  auto k = checksum_kernel_dma<LPF, NCH, R>;
+  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kTile)), dim3(kBlock), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_dma launch");
 }
 
