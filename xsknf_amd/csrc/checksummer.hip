@@ -88,6 +88,10 @@ __device__ __forceinline__ void lds_store_i32(uint32_t a, int32_t v) {
   *reinterpret_cast<__attribute__((address_space(3))) int32_t *>(static_cast<uintptr_t>(a)) = v;
 }
 
+__device__ __forceinline__ void lds_store_u32(uint32_t a, uint32_t v) {
+  *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(static_cast<uintptr_t>(a)) = v;
+}
+
 __device__ __forceinline__ int32_t lds_i32(uint32_t a) {
   return *reinterpret_cast<const __attribute__((address_space(3))) int32_t *>(static_cast<uintptr_t>(a));
 }
@@ -273,17 +277,59 @@ __device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const Frame
   return verdict;
 }
 
-// Frames longer than one pass: the remaining passes as direct loads.
+// Frames longer than one pass.  The pipelined step only sums pass 0 and parks
+// the frame as PENDING (tag 10 in bits 31..30 of its result word, u below, the
+// partial sum pseudo + mult*(P0 - old_check) in part[i]); the remaining passes
+// run at the end of the tile, when no prefetch buffer is live (keeping them in
+// the step would cost ~60 VGPRs of occupancy for a rare case).
+constexpr uint32_t kPendTag = 0x80000000u;
+
+// Result word of a frame after its pass-0 sum P0 (group-reduced, last lane).
+__device__ __forceinline__ int32_t step_result(const KernelArgs &a, const FrameRef &r, const Header &h,
+                                               int32_t verdict, bool do_sum, uint32_t P0, int span,
+                                               uint32_t part_addr) {
+  if (do_sum && r.nch > span) {
+    lds_store_u32(part_addr, h.pseudo + a.payload_mult * (P0 - h.old_check));
+    return static_cast<int32_t>(kPendTag | static_cast<uint32_t>(h.u));
+  }
+  return frame_result(a, r, h, verdict, do_sum, P0);
+}
+
+// Finish the PENDING frames of a tile: passes 1.. of each, then their result.
+// dsc: the tile's descriptors in LDS; rec / part: the tile's result words and
+// partial sums in LDS (index step * G + group).
 template <int LPF, int NCH>
-__device__ __forceinline__ void tail_passes(const FrameRef &r, int gl, int lo, int hi, uint32_t wl,
-                                            uint32_t wh, uint32_t &acc_lo, uint32_t &acc_hi) {
+__device__ __forceinline__ void finish_long_frames(const KernelArgs &a, uint32_t dsc, uint32_t tf0, uint32_t rec,
+                                                uint32_t part, int steps, int grp, int gl) {
+  constexpr int G = kWave / LPF;
   constexpr int SPAN = LPF * NCH;
-  for (int p = SPAN; p < r.nch; p += SPAN) {
-    uint4 t[NCH];
+  for (int st = 0; st < steps; ++st) {
+    const uint32_t i = st * G + grp;
+    const uint32_t rv = static_cast<uint32_t>(lds_i32(rec + 4 * i));
+    const bool pend = (rv & kRecTagMask) == kPendTag && tf0 + i < a.n;
+    if (!__builtin_amdgcn_ballot_w64(pend)) continue;
+    const FrameRef r = ref_from_lds(a, dsc + 16 * i, tf0 + i);
+    const int u = static_cast<int>(rv & 0x7f);
+    const int lo = r.rs + u, hi = pend ? r.rs + r.len : lo;   // idle groups sum nothing
+    const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+    const uint32_t wh = wl << 8 | wl >> 24;
+    uint32_t acc_lo = 0, acc_hi = 0;
+    for (int p = SPAN; __builtin_amdgcn_ballot_w64(pend && p < r.nch); p += SPAN) {
+      uint4 t[NCH];
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) t[k] = load_nt(r.cp + min(p + k * LPF + gl, r.nch - 1));
+      for (int k = 0; k < NCH; ++k) t[k] = load_nt(r.cp + min(p + k * LPF + gl, r.nch - 1));
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) chunk_sum(t[k], (p + k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+      for (int k = 0; k < NCH; ++k) chunk_sum_fast(t[k], (p + k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
+    }
+    const uint32_t Prest = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
+    if (gl == LPF - 1 && pend) {
+      const uint32_t sum = lds_i32(part + 4 * i) + a.payload_mult * Prest;   // :92-103
+      const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((sum & 0xffffu) + (sum >> 16)));
+      int32_t res = a.fwd_verdict;
+      if (a.defer) res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(u) << 16) | c);
+      else *reinterpret_cast<uint16_t *>(r.fp + u + 6) = c;   // :108
+      lds_store_i32(rec + 4 * i, res);
+    }
   }
 }
 
@@ -311,7 +357,7 @@ __device__ __forceinline__ void load_frame(const FrameRef &r, int gl, uint4 (&v)
 
 template <int LPF, int NCH>
 __device__ __forceinline__ int32_t process_regs(const KernelArgs &args, const FrameRef &r, const uint4 (&v)[NCH],
-                                                uint32_t slot, int gl, uint32_t &P) {
+                                                uint32_t slot, int gl, uint32_t part_addr) {
   // header window (chunks 0..6) to LDS; one wave's LDS accesses execute in issue
   // order, only the compiler must not move the reads above the writes
 #pragma unroll
@@ -330,9 +376,8 @@ __device__ __forceinline__ int32_t process_regs(const KernelArgs &args, const Fr
   uint32_t acc_lo = 0, acc_hi = 0;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) chunk_sum_fast(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-  if (do_sum) tail_passes<LPF, NCH>(r, gl, lo, hi, wl, wh, acc_lo, acc_hi);
-  P = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
-  return (gl == LPF - 1 && r.exists) ? frame_result(args, r, h, verdict, do_sum, P) : 0;
+  const uint32_t P0 = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
+  return (gl == LPF - 1 && r.exists) ? step_result(args, r, h, verdict, do_sum, P0, LPF * NCH, part_addr) : 0;
 }
 
 template <int LPF, int NCH, int SPT>
@@ -345,6 +390,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
 
   __shared__ __attribute__((aligned(16))) uint8_t hdr[kWavesPerBlock][G][kSlotBytes];
   __shared__ __attribute__((aligned(16))) int32_t recs[kWavesPerBlock][kWave];
+  __shared__ __attribute__((aligned(16))) uint32_t parts[kWavesPerBlock][kWave];
   __shared__ __attribute__((aligned(16))) xsknf_gpu_desc dtile[kWavesPerBlock][kWave];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -353,6 +399,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
   const int gl = lane % LPF;
   const uint32_t slot = lds_addr(&hdr[wv][grp][0]);
   const uint32_t rec = lds_addr(&recs[wv][0]);
+  const uint32_t part = lds_addr(&parts[wv][0]);
   const uint32_t dsc = lds_addr(&dtile[wv][0]);
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t last = args.n - 1;
@@ -382,11 +429,12 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
         rn = ref_from_lds(args, dsc + 16 * i, tf0 + i);
         load_frame<LPF, NCH>(rn, gl, vn);
       }
-      uint32_t P;
-      const int32_t res = process_regs<LPF, NCH>(args, rc, vc, slot, gl, P);
+      const int32_t res = process_regs<LPF, NCH>(args, rc, vc, slot, gl, part + 4 * (st * G + grp));
       if (gl == LPF - 1 && rc.exists) lds_store_i32(rec + 4 * (st * G + grp), res);
       compiler_barrier();   // the next frame rewrites this group's header window
     }
+    compiler_barrier();
+    finish_long_frames<LPF, NCH>(args, dsc, tf0, rec, part, SPT, grp, gl);
     compiler_barrier();
     if (lane < T && tf0 + lane < args.n) args.verdicts[tf0 + lane] = lds_i32(rec + 4 * lane);
     compiler_barrier();
@@ -412,7 +460,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
 
 __device__ __forceinline__ void dma16_nt(const void *gaddr, uint32_t lds) {
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt"
-               :: "v"(gaddr), "s"(lds) : "memory", "m0");
+               :: "v"(gaddr), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
 }
 
 template <int N>
@@ -432,6 +480,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
 
   __shared__ __attribute__((aligned(1024))) uint8_t ring[kWavesPerBlock][R][SLOT];
   __shared__ __attribute__((aligned(16))) int32_t recs[kWavesPerBlock][kTile];
+  __shared__ __attribute__((aligned(16))) uint32_t parts[kWavesPerBlock][kTile];
   __shared__ __attribute__((aligned(1024))) xsknf_gpu_desc dtile[kWavesPerBlock][2][kTile];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -440,6 +489,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
   const int gl = lane % LPF;
   const uint32_t ring0 = lds_addr(&ring[wv][0][0]);
   const uint32_t rec = lds_addr(&recs[wv][0]);
+  const uint32_t part = lds_addr(&parts[wv][0]);
   const uint32_t dsc0 = lds_addr(&dtile[wv][0][0]);
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t wg = blockIdx.x * kWavesPerBlock + wv;
@@ -501,11 +551,15 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
       uint32_t acc_lo = 0, acc_hi = 0;
 #pragma unroll
       for (int k = 0; k < NCH; ++k) chunk_sum_fast(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-      if (do_sum) tail_passes<LPF, NCH>(r, gl, lo, hi, wl, wh, acc_lo, acc_hi);
-      const uint32_t P = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
+      const uint32_t P0 = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
       if (gl == LPF - 1 && r.exists)
-        lds_store_i32(rec + 4 * (js * G + grp), frame_result(args, r, h, verdict, do_sum, P));
-      if (js == SPT - 1) flush_tile(args, rec, f0, lane);   // steps past n ran as no-ops
+        lds_store_i32(rec + 4 * (js * G + grp),
+                      step_result(args, r, h, verdict, do_sum, P0, LPF * NCH, part + 4 * (js * G + grp)));
+      if (js == SPT - 1) {             // steps past n ran as no-ops
+        compiler_barrier();
+        finish_long_frames<LPF, NCH>(args, dsc0 + (tk & 1) * (kTile * 16), f0, rec, part, SPT, grp, gl);
+        flush_tile(args, rec, f0, lane);
+      }
       ++j;
     }
   }
