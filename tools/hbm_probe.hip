@@ -42,6 +42,16 @@ __global__ __launch_bounds__(256) void probe(uint8_t *__restrict__ base, uint64_
         const uint64_t c = j / ppc, p = j % ppc;
         // the checksummer's stores: 2 bytes at frame byte 40 (piece 2), 4 B verdict (piece 0)
         if (wr_check == 1 && p == 2) *reinterpret_cast<uint16_t *>(base + c * stride + off + 40) = (uint16_t)v[k].x;
+        if (wr_check == -2 && p == 2)
+          __builtin_nontemporal_store((uint16_t)v[k].x, reinterpret_cast<uint16_t *>(base + c * stride + off + 40));
+        if (wr_check == -64) {   // nt rewrite of the 64-B sector holding byte 40, by the lanes holding it
+          const uint64_t a = c * stride + off + 40;
+          const uint64_t blk = a & ~(uint64_t)63;
+          const uint64_t me = c * stride + off + p * 16;
+          typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+          const u4v x = {v[k].x, v[k].y, v[k].z, v[k].w};
+          if (me >= blk && me < blk + 64) __builtin_nontemporal_store(x, reinterpret_cast<u4v *>(base + me));
+        }
         // wr_check = B > 1: rewrite the whole aligned B-byte block holding frame byte 40
         if (wr_check > 1) {
           const uint64_t a = c * stride + off + 40;
@@ -134,6 +144,45 @@ __global__ __launch_bounds__(256) void scatter(uint8_t *__restrict__ base, uint6
     *reinterpret_cast<uint16_t *>(base + c * stride + off + 40) = (uint16_t)vals[c];
 }
 
+// write-only pass with non-temporal stores
+__global__ __launch_bounds__(256) void scatter_nt(uint8_t *__restrict__ base, uint64_t chunks,
+                                                  uint32_t stride, uint32_t off,
+                                                  const uint32_t *__restrict__ vals) {
+  for (uint64_t c = blockIdx.x * 256ull + threadIdx.x; c < chunks; c += gridDim.x * 256ull)
+    __builtin_nontemporal_store((uint16_t)vals[c], reinterpret_cast<uint16_t *>(base + c * stride + off + 40));
+}
+
+// write-only pass rewriting the whole aligned B-byte sector holding byte off+40 (nt)
+template <int B>
+__global__ __launch_bounds__(256) void scatter_sector(uint8_t *__restrict__ base, uint64_t chunks,
+                                                      uint32_t stride, uint32_t off,
+                                                      const uint32_t *__restrict__ vals) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  for (uint64_t c = blockIdx.x * 256ull + threadIdx.x; c < chunks; c += gridDim.x * 256ull) {
+    uint8_t *sec = base + ((c * stride + off + 40) & ~(uint64_t)(B - 1));
+    const u4v v = {vals[c], 1u, 2u, 3u};
+#pragma unroll
+    for (int k = 0; k < B / 16; ++k) __builtin_nontemporal_store(v, reinterpret_cast<u4v *>(sec + 16 * k));
+  }
+}
+
+// same, but L lanes per chunk, each storing one 16-B piece of the B = 16*L sector
+// in the SAME store instruction (so the pieces coalesce into one full-sector write)
+template <int L>
+__global__ __launch_bounds__(256) void scatter_coal(uint8_t *__restrict__ base, uint64_t chunks,
+                                                    uint32_t stride, uint32_t off,
+                                                    const uint32_t *__restrict__ vals) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  const uint64_t t0 = blockIdx.x * 256ull + threadIdx.x;
+  for (uint64_t t = t0; t < chunks * L; t += gridDim.x * 256ull) {
+    const uint64_t c = t / L;
+    const int piece = t % L;
+    uint8_t *sec = base + ((c * stride + off + 40) & ~(uint64_t)(16 * L - 1));
+    const u4v v = {vals[c], 1u, 2u, 3u};
+    __builtin_nontemporal_store(v, reinterpret_cast<u4v *>(sec + 16 * piece));
+  }
+}
+
 int main(int argc, char **argv) {
   if (argc < 5) { fprintf(stderr, "usage: %s chunks stride off len [reps]\n", argv[0]); return 2; }
   const uint64_t chunks = strtoull(argv[1], 0, 0);
@@ -195,6 +244,35 @@ int main(int argc, char **argv) {
       const double us2 = ms2 * 1e3 / reps;
       printf("{\"mode\": \"tiled\", \"tile\": %u, \"len\": %u, \"us\": %.2f, \"read_GBps\": %.1f}\n",
              tl, len, us2, rd / us2 / 1e3);
+    }
+  }
+  if (getenv("PROBE_SEQ")) {
+    // alternate an nt read pass with a scatter pass; time each separately
+    for (int mode = 0; mode < 9; ++mode) {   // 0: none, 1: plain 2B, 2: nt 2B, 3: nt 16B, 4: nt 32B, 5: nt 64B, 6/7/8: 2/4/8 lanes x 16B coalesced
+      double rsum = 0, ssum = 0;
+      for (int r = 0; r < reps; ++r) {
+        hipEvent_t a0, a1, a2;
+        CHECK(hipEventCreate(&a0)); CHECK(hipEventCreate(&a1)); CHECK(hipEventCreate(&a2));
+        CHECK(hipEventRecord(a0));
+        hipLaunchKernelGGL(probe_mode<1>, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out);
+        CHECK(hipEventRecord(a1));
+        if (mode == 1) hipLaunchKernelGGL(scatter, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        if (mode == 2) hipLaunchKernelGGL(scatter_nt, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        if (mode == 3) hipLaunchKernelGGL(scatter_sector<16>, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        if (mode == 4) hipLaunchKernelGGL(scatter_sector<32>, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        if (mode == 5) hipLaunchKernelGGL(scatter_sector<64>, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        if (mode == 6) hipLaunchKernelGGL(scatter_coal<2>, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        if (mode == 7) hipLaunchKernelGGL(scatter_coal<4>, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        if (mode == 8) hipLaunchKernelGGL(scatter_coal<8>, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        CHECK(hipEventRecord(a2));
+        CHECK(hipEventSynchronize(a2));
+        float t1 = 0, t2 = 0;
+        CHECK(hipEventElapsedTime(&t1, a0, a1));
+        CHECK(hipEventElapsedTime(&t2, a1, a2));
+        if (r > 0) { rsum += t1; ssum += t2; }
+      }
+      printf("{\"seq_mode\": %d, \"read_us\": %.2f, \"scatter_us\": %.2f}\n", mode,
+             rsum * 1e3 / (reps - 1), ssum * 1e3 / (reps - 1));
     }
   }
   if (getenv("PROBE_SCATTER")) {

@@ -565,16 +565,60 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
   }
 }
 
-// ---- phase 2: write-only scatter of the parked checks (:108) and verdicts ----
+// ---- phase 2: write-only pass of the parked checks (:108) and verdicts -------
+//
+// Measured on MI355X (tools/hbm_probe): a scattered 2-byte write costs as much
+// as a read-modify-write of its 64-byte memory sector, and writes left dirty in
+// the caches are written back during the NEXT batch's read pass, where they
+// cost far more.  So this pass uses non-temporal stores (written back now) and,
+// where the aligned 64-byte sector holding the check lies entirely inside the
+// frame, rewrites the whole sector -- its 64 bytes re-read and patched -- as ONE
+// store instruction of 4 adjacent lanes (a full-sector write, no RMW): 4 lanes
+// per frame.  Otherwise (sector crosses the frame edge, or the check straddles
+// two sectors) it writes the 2 check bytes alone.  Only this frame's own bytes
+// are ever rewritten (with their own values), so frames never race.
+
+__device__ __forceinline__ void store_nt16(uint8_t *p, uint4 v) {
+  u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
+}
 
 __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) {
-  for (uint32_t f = blockIdx.x * kBlock + threadIdx.x; f < args.n; f += gridDim.x * kBlock) {
+  const uint32_t nthreads = gridDim.x * kBlock;
+  for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < 4 * args.n; t += nthreads) {
+    const uint32_t f = t >> 2;
+    const int piece = t & 3;
     const uint32_t r = static_cast<uint32_t>(args.verdicts[f]);
-    if ((r & kRecTagMask) == kRecTag) {
-      const uint64_t off = umem_offset(args.descs[f].addr);
-      *reinterpret_cast<uint16_t *>(args.umem + off + ((r >> 16) & 0x7f) + 6) = static_cast<uint16_t>(r);
-      args.verdicts[f] = args.fwd_verdict;
+    if ((r & kRecTagMask) != kRecTag) continue;
+    const xsknf_gpu_desc d = args.descs[f];
+    uint8_t *fp = args.umem + umem_offset(d.addr);
+    uint8_t *chk = fp + ((r >> 16) & 0x7f) + 6;
+    const uint16_t c = static_cast<uint16_t>(r);
+    uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);   // keeps global addressing
+    const bool whole = sec >= fp && sec + 64 <= fp + d.len && (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
+    if (whole) {
+      uint8_t *mine = sec + 16 * piece;
+      uint4 v = load_nt(reinterpret_cast<const uint4 *>(mine));
+      const int o = static_cast<int>(chk - mine);          // check offset in my 16-B piece
+      if (o >= 0 && o < 16) {                              // low byte here (high byte too unless o == 15)
+        uint8_t b[16];
+        memcpy(b, &v, 16);
+        b[o] = static_cast<uint8_t>(c);
+        if (o + 1 < 16) b[o + 1] = static_cast<uint8_t>(c >> 8);
+        memcpy(&v, b, 16);
+      }
+      if (o == -1) {                                       // high byte lands at my first byte
+        uint8_t b[16];
+        memcpy(b, &v, 16);
+        b[0] = static_cast<uint8_t>(c >> 8);
+        memcpy(&v, b, 16);
+      }
+      store_nt16(mine, v);
+    } else if (piece == 0) {
+      chk[0] = static_cast<uint8_t>(c);
+      chk[1] = static_cast<uint8_t>(c >> 8);
     }
+    if (piece == 0) args.verdicts[f] = args.fwd_verdict;
   }
 }
 
@@ -630,7 +674,7 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
 int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && a.defer) {
-    const uint32_t need = (a.n + kBlock - 1) / kBlock;
+    const uint32_t need = (4 * a.n + kBlock - 1) / kBlock;
     const uint32_t cap = static_cast<uint32_t>(device_cus() * 8);
     hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
     e = hipGetLastError();
@@ -687,7 +731,9 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.blocks_per_cu = 8;
   c.fused_stores = 0;
   c.lds_ring = 0;
-  if (hint + 15 <= 128) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.frames_per_group = 4; }
+  // small frames: the check write hits the line the frame was just read from, so
+  // in-line stores are cheaper than a second pass (tools/hbm_probe)
+  if (hint + 15 <= 128) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.frames_per_group = 4; c.fused_stores = 1; }
   else if (hint + 15 <= 512) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 4; }
   else if (hint + 15 <= 1536) { c.lanes_per_frame = 32; c.chunks_per_lane = 3; c.frames_per_group = 4; }
   else if (hint + 15 <= 4096) { c.lanes_per_frame = 64; c.chunks_per_lane = 4; c.frames_per_group = 4; }
