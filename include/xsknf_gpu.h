@@ -92,10 +92,12 @@ int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * 256-thread blocks per CU (0 = 8).  `lds_ring` > 0 selects the LDS-DMA
  * kernel, which streams each wave's frames through a ring of that many LDS
  * slots (frames_per_group is then ignored); 0 selects the register kernel.
- * `fused_stores` = 1 writes the check bytes from the summing kernel itself;
- * 0 (default) parks them and writes them in a second, write-only pass, which is
- * faster on MI355X (scattered writes mixed into the read stream cost ~25 % of
- * the read bandwidth).  Only instantiated shapes are accepted (-EINVAL
+ * `fused_stores` = 1 writes every check from the summing kernel itself; 2 parks
+ * every check for a second, write-only pass (non-temporal full 64-byte sector
+ * rewrites); 0 (default) decides per frame: frames of 256 bytes or more are
+ * deferred (scattered writes mixed into the read stream cost ~25 % of its
+ * bandwidth on MI355X), shorter ones write in-line (their check shares the line
+ * just read).  Only instantiated shapes are accepted (-EINVAL
  * otherwise); every shape gives identical results.
  */
 struct xsknf_gpu_launch_cfg {

@@ -170,7 +170,8 @@ struct KernelArgs {
   uint32_t n;
   uint32_t payload_mult;   // max(csum_iterations, 0)
   int32_t fwd_verdict;     // REDIRECT ? (ingress+1) % n_if : -1
-  uint32_t defer;          // 1: park check records in `verdicts`, scatter in a 2nd pass
+  uint32_t defer_min_len;  // frames at least this long park a check record for the
+                           // scatter pass; shorter ones write their check in-line
   const uint4 *dummy;      // readable 16-byte block for frames that need no bytes
 };
 
@@ -272,7 +273,8 @@ __device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const Frame
                                                 int32_t verdict, bool do_sum, uint32_t P) {
   if (!do_sum) return verdict;
   const uint16_t c = check_of(h, P, a.payload_mult);
-  if (a.defer) return static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
+  if (static_cast<uint32_t>(r.len) >= a.defer_min_len)
+    return static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
   *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
   return verdict;
 }
@@ -283,6 +285,9 @@ __device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const Frame
 // run at the end of the tile, when no prefetch buffer is live (keeping them in
 // the step would cost ~60 VGPRs of occupancy for a rare case).
 constexpr uint32_t kPendTag = 0x80000000u;
+constexpr uint32_t kNoDefer = 0xffffffffu;     // defer_min_len: every check in-line
+constexpr uint32_t kDeferMinLen = 256;         // hybrid default (tools/tune.py: 64 B and
+                                               // IMIX prefer in-line, 1500 B deferred)
 
 // Result word of a frame after its pass-0 sum P0 (group-reduced, last lane).
 __device__ __forceinline__ int32_t step_result(const KernelArgs &a, const FrameRef &r, const Header &h,
@@ -326,7 +331,8 @@ __device__ __forceinline__ void finish_long_frames(const KernelArgs &a, uint32_t
       const uint32_t sum = lds_i32(part + 4 * i) + a.payload_mult * Prest;   // :92-103
       const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((sum & 0xffffu) + (sum >> 16)));
       int32_t res = a.fwd_verdict;
-      if (a.defer) res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(u) << 16) | c);
+      if (static_cast<uint32_t>(r.len) >= a.defer_min_len)
+        res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(u) << 16) | c);
       else *reinterpret_cast<uint16_t *>(r.fp + u + 6) = c;   // :108
       lds_store_i32(rec + 4 * i, res);
     }
@@ -673,7 +679,7 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
 
 int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess && a.defer) {
+  if (e == hipSuccess && a.defer_min_len != kNoDefer) {
     const uint32_t need = (4 * a.n + kBlock - 1) / kBlock;
     const uint32_t cap = static_cast<uint32_t>(device_cus() * 8);
     hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
@@ -733,9 +739,9 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.lds_ring = 0;
   // small frames: the check write hits the line the frame was just read from, so
   // in-line stores are cheaper than a second pass (tools/hbm_probe)
-  if (hint + 15 <= 128) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.frames_per_group = 4; c.fused_stores = 1; }
+  if (hint + 15 <= 128) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.frames_per_group = 4; }
   else if (hint + 15 <= 512) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 4; }
-  else if (hint + 15 <= 1536) { c.lanes_per_frame = 32; c.chunks_per_lane = 3; c.frames_per_group = 4; }
+  else if (hint + 15 <= 1536) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 4; }
   else if (hint + 15 <= 4096) { c.lanes_per_frame = 64; c.chunks_per_lane = 4; c.frames_per_group = 4; }
   else { c.lanes_per_frame = 64; c.chunks_per_lane = 9; c.frames_per_group = 4; }
 }
@@ -756,7 +762,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
   a.fwd_verdict = opts->action == XSKNF_CSUM_ACTION_REDIRECT
                       ? static_cast<int32_t>((ingress_ifindex + 1u) % opts->num_interfaces)
                       : -1;
-  a.defer = 1;
+  a.defer_min_len = kDeferMinLen;
   // aligned-down descriptor address: inside the descriptor array's own page
   a.dummy = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(descs) & ~static_cast<uintptr_t>(15));
   return 0;
@@ -764,11 +770,11 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
 
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
-  if (cfg.fused_stores != 0 && cfg.fused_stores != 1) return -EINVAL;
+  if (cfg.fused_stores < 0 || cfg.fused_stores > 2) return -EINVAL;
   const Variant *v = find_variant(cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group, cfg.lds_ring);
   if (!v) return -EINVAL;
   KernelArgs a = base;
-  a.defer = cfg.fused_stores ? 0u : 1u;
+  a.defer_min_len = cfg.fused_stores == 1 ? kNoDefer : (cfg.fused_stores == 2 ? 0u : kDeferMinLen);
   return v->fn(a, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
 }
 
