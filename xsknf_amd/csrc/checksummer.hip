@@ -286,8 +286,8 @@ __device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const Frame
 // the step would cost ~60 VGPRs of occupancy for a rare case).
 constexpr uint32_t kPendTag = 0x80000000u;
 constexpr uint32_t kNoDefer = 0xffffffffu;     // defer_min_len: every check in-line
-constexpr uint32_t kDeferMinLen = 256;         // hybrid default (tools/tune.py: 64 B and
-                                               // IMIX prefer in-line, 1500 B deferred)
+constexpr uint32_t kDeferMinLen = 1024;        // hybrid default (tools/tune.py: 64 B, 570 B
+                                               // and IMIX prefer in-line, 1500 B deferred)
 
 // Result word of a frame after its pass-0 sum P0 (group-reduced, last lane).
 __device__ __forceinline__ int32_t step_result(const KernelArgs &a, const FrameRef &r, const Header &h,
@@ -730,18 +730,17 @@ const Variant *find_variant(int lpf, int nch, int u, int ring) {
   return nullptr;
 }
 
-// Default shape for a length hint: one pass covers hint + 15 bytes of 16-byte
-// misalignment (measured best per size class, tools/tune.py).
+// Default shape for a length hint.
 void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.frames_per_group = 1;
   c.blocks_per_cu = 8;
   c.fused_stores = 0;
   c.lds_ring = 0;
-  // small frames: the check write hits the line the frame was just read from, so
-  // in-line stores are cheaper than a second pass (tools/hbm_probe)
-  if (hint + 15 <= 128) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.frames_per_group = 4; }
-  else if (hint + 15 <= 512) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 4; }
-  else if (hint + 15 <= 1536) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 4; }
+  // measured best per size class on MI355X (tools/tune.py, 1M-frame batches):
+  // up to ~1 KiB, 8 lanes per frame (longer frames finish their extra passes at
+  // tile end); 1500 B, 16 lanes x 2 chunks; jumbo frames, one wave per frame
+  if (hint <= 1024) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.frames_per_group = 4; }
+  else if (hint + 15 <= 2048) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 4; }
   else if (hint + 15 <= 4096) { c.lanes_per_frame = 64; c.chunks_per_lane = 4; c.frames_per_group = 4; }
   else { c.lanes_per_frame = 64; c.chunks_per_lane = 9; c.frames_per_group = 4; }
 }
