@@ -28,6 +28,9 @@
 extern "C" {
 #endif
 
+/* Everything else in the library is hidden (built with -fvisibility=hidden). */
+#define XSKNF_GPU_API __attribute__((visibility("default")))
+
 /* Same layout as struct xdp_desc (linux/if_xdp.h), i.e. exactly what the rx
  * ring holds and what xsk_ring_cons__rx_desc() returns (src/xsknf.c:655-656). */
 struct xsknf_gpu_desc {
@@ -53,10 +56,10 @@ struct xsknf_csum_opts {
 };
 
 /* Library version: (major << 16) | minor. */
-uint32_t xsknf_gpu_version(void);
+XSKNF_GPU_API uint32_t xsknf_gpu_version(void);
 
 /* Number of visible HIP devices in *count. */
-int xsknf_gpu_device_count(int *count);
+XSKNF_GPU_API int xsknf_gpu_device_count(int *count);
 
 /*
  * Checksum one rx batch, asynchronously on `stream`, on the current HIP device.
@@ -77,7 +80,7 @@ int xsknf_gpu_device_count(int *count);
  * reference never sees one).
  * Returns 0, -EINVAL on bad arguments, -EIO on a HIP launch error.
  */
-int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
+XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
 		const struct xsknf_gpu_desc *descs, uint32_t n,
 		uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
 		int32_t *verdicts, uint32_t frame_len_hint, void *stream);
@@ -110,16 +113,54 @@ struct xsknf_gpu_launch_cfg {
 };
 
 /* The shape xsknf_gpu_checksum_batch() uses for a given frame_len_hint. */
-int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg);
+XSKNF_GPU_API int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg);
 
 /* xsknf_gpu_checksum_batch() with an explicit launch shape instead of a hint. */
-int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size,
+XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size,
 		const struct xsknf_gpu_desc *descs, uint32_t n,
 		uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
 		int32_t *verdicts, const struct xsknf_gpu_launch_cfg *cfg, void *stream);
 
+/*
+ * Host-path context: the batch hook as the AF_XDP worker of src/xsknf.c would
+ * call it, with the UMEM in host memory (the worker's mmap, src/xsknf.c:958,975)
+ * and descriptors / verdicts in host arrays (the rx ring and to_drop / to_tx
+ * routing of process_batch_1if, src/xsknf.c:654-672).
+ *
+ *   XSKNF_GPU_PATH_ZEROCOPY  the UMEM is pinned and mapped; the kernel reads
+ *                            the frames and writes the check bytes in place
+ *                            over PCIe (no copies).
+ *   XSKNF_GPU_PATH_STAGED    the byte span of each batch is copied to a device
+ *                            mirror (hipMemcpyAsync from the pinned UMEM),
+ *                            checksummed in HBM and copied back.
+ * One context = one worker thread = one HIP stream.  Calls are synchronous:
+ * when xsknf_gpu_ctx_process_batch() returns, verdicts and check bytes are in
+ * host memory.
+ */
+#define XSKNF_GPU_PATH_ZEROCOPY 0
+#define XSKNF_GPU_PATH_STAGED 1
+
+struct xsknf_gpu_ctx;
+
+struct xsknf_gpu_ctx_stats {
+	uint64_t batches;
+	uint64_t frames;
+	uint64_t bytes_h2d;
+	uint64_t bytes_d2h;
+};
+
+XSKNF_GPU_API int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **ctx, int device, int path,
+		uint32_t max_batch, uint32_t frame_len_hint);
+/* Pin (and for ZEROCOPY map) the host UMEM [umem, umem + size). */
+XSKNF_GPU_API int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *ctx, void *umem, uint64_t size);
+XSKNF_GPU_API int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *ctx,
+		const struct xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
+		const struct xsknf_csum_opts *opts, int32_t *verdicts);
+XSKNF_GPU_API int xsknf_gpu_ctx_get_stats(const struct xsknf_gpu_ctx *ctx, struct xsknf_gpu_ctx_stats *stats);
+XSKNF_GPU_API int xsknf_gpu_ctx_destroy(struct xsknf_gpu_ctx *ctx);
+
 /* Text of the last HIP error seen by this library on the calling thread. */
-const char *xsknf_gpu_last_error(void);
+XSKNF_GPU_API const char *xsknf_gpu_last_error(void);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -72,3 +72,20 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.XsknfGpuError):
         _lib.load()
+
+
+def test_only_declared_symbols_are_exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert exported == set(declared_functions())
+
+
+def test_ctx_argument_validation_without_gpu():
+    lib = _lib.load()
+    ctx = ctypes.c_void_p()
+    assert lib.xsknf_gpu_ctx_create(None, 0, 0, 16, 0) == -errno.EINVAL
+    assert lib.xsknf_gpu_ctx_create(ctypes.byref(ctx), 0, 7, 16, 0) == -errno.EINVAL
+    assert lib.xsknf_gpu_ctx_create(ctypes.byref(ctx), 0, 0, 0, 0) == -errno.EINVAL
+    assert lib.xsknf_gpu_ctx_process_batch(None, None, 0, 0, None, None) == -errno.EINVAL
+    assert lib.xsknf_gpu_ctx_destroy(None) == -errno.EINVAL

@@ -205,3 +205,24 @@ def test_every_launch_shape_is_bit_exact(dev, shape, layout):
     torch.cuda.synchronize()
     assert np.array_equal(v.cpu().numpy(), ov)
     assert np.array_equal(umem.cpu().numpy(), ou)
+
+
+@pytest.mark.parametrize("path", ["zerocopy", "staged"])
+@pytest.mark.parametrize("layout", ["aligned", "unaligned"])
+def test_host_path_bit_exact(dev, path, layout):
+    """UMEM in (pinned) host memory, descriptors / verdicts in host arrays."""
+    from xsknf_amd import HostPath
+    b = (frames.aligned_batch(3000, "imix", chunk=2048) if layout == "aligned"
+         else frames.unaligned_batch(3000, "imix"))
+    frames.inject_edge_cases(b, 0.1)
+    ou, ov = run_oracle(b, iters=3, action=O.REDIRECT, nif=2, ingress=1)
+    cs = Checksummer(ChecksummerOptions(action=O.REDIRECT, csum_iterations=3), num_interfaces=2,
+                     frame_len_hint=1500)
+    umem = b.umem.copy()
+    with HostPath(cs, umem, path=path, max_batch=4096) as hp:
+        v = np.concatenate([hp.process_batch(b.descs[i:i + 700], ingress_ifindex=1)
+                            for i in range(0, b.n, 700)])
+        st = hp.stats()
+    assert st["frames"] == b.n
+    assert np.array_equal(v, ov)
+    assert np.array_equal(umem, ou)

@@ -2,8 +2,10 @@
 """HBM traffic per hot-path step from rocprofv3 --pmc passes (tools/prof_pmc.sh).
 
 gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE reports exactly half of
-the bytes of a wide coalesced streaming read, so fetched bytes = 2 x FETCH_SIZE
-(KiB); WRITE_SIZE reads bytes exactly for 16-B-per-lane streaming stores.
+the bytes of a wide coalesced streaming read, so the summing kernel's fetched
+bytes = 2 x FETCH_SIZE (KiB); the scatter pass's sector / word reads are taken
+1:1 (they match its byte count); WRITE_SIZE reads bytes exactly for 16-B
+streaming stores.
 A step of the hot path = the summing kernel + the scatter kernel; their
 per-dispatch means are added.
 
@@ -36,7 +38,9 @@ def main():
     d, workload = sys.argv[1], sys.argv[2]
     fetch = per_kernel(d, "FETCH_SIZE")
     write = per_kernel(d, "WRITE_SIZE")
-    fetch_b = sum(2 * 1024 * v for v in fetch.values())
+    # the 2x correction holds for wide coalesced streaming reads (the summing
+    # kernel); the scatter pass reads 64-B sectors and 4-16 B words, counted 1:1
+    fetch_b = sum((2 if "checksum_kernel" in k else 1) * 1024 * v for k, v in fetch.items())
     write_b = sum(1024 * v for v in write.values())
     out = {
         "workload": workload,
@@ -44,7 +48,8 @@ def main():
         "fetch_bytes": int(fetch_b), "write_bytes": int(write_b),
         "per_kernel_fetch_KiB_raw": fetch, "per_kernel_write_KiB_raw": write,
         "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py; "
-                  "fetch = 2 x FETCH_SIZE (gfx950 half-count correction), write = WRITE_SIZE; "
+                  "fetch = 2 x FETCH_SIZE for the streaming summing kernel (gfx950 half-count "
+                  "correction), 1 x for the scatter pass; write = WRITE_SIZE; "
                   "per dispatch, summing + scatter kernels of one step",
     }
     print(json.dumps(out, indent=1))

@@ -20,7 +20,15 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_last_error",
     "xsknf_gpu_default_launch_cfg",
     "xsknf_gpu_checksum_batch_cfg",
+    "xsknf_gpu_ctx_create",
+    "xsknf_gpu_ctx_register_umem",
+    "xsknf_gpu_ctx_process_batch",
+    "xsknf_gpu_ctx_get_stats",
+    "xsknf_gpu_ctx_destroy",
 )
+
+PATH_ZEROCOPY = 0
+PATH_STAGED = 1
 
 ACTION_REDIRECT = 0
 ACTION_DROP = 1
@@ -48,6 +56,13 @@ class LaunchCfg(ctypes.Structure):
         ("lds_ring", ctypes.c_int32),
         ("fused_stores", ctypes.c_int32),
     ]
+
+
+class CtxStats(ctypes.Structure):
+    """struct xsknf_gpu_ctx_stats (include/xsknf_gpu.h)."""
+
+    _fields_ = [("batches", ctypes.c_uint64), ("frames", ctypes.c_uint64),
+                ("bytes_h2d", ctypes.c_uint64), ("bytes_d2h", ctypes.c_uint64)]
 
 
 class XsknfGpuError(RuntimeError):
@@ -90,6 +105,19 @@ def load() -> ctypes.CDLL:
         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.POINTER(CsumOpts), ctypes.c_void_p, ctypes.POINTER(LaunchCfg), ctypes.c_void_p,
     ]
+    lib.xsknf_gpu_ctx_create.restype = ctypes.c_int
+    lib.xsknf_gpu_ctx_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_uint32, ctypes.c_uint32]
+    lib.xsknf_gpu_ctx_register_umem.restype = ctypes.c_int
+    lib.xsknf_gpu_ctx_register_umem.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    lib.xsknf_gpu_ctx_process_batch.restype = ctypes.c_int
+    lib.xsknf_gpu_ctx_process_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                ctypes.c_uint32, ctypes.POINTER(CsumOpts),
+                                                ctypes.c_void_p]
+    lib.xsknf_gpu_ctx_get_stats.restype = ctypes.c_int
+    lib.xsknf_gpu_ctx_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(CtxStats)]
+    lib.xsknf_gpu_ctx_destroy.restype = ctypes.c_int
+    lib.xsknf_gpu_ctx_destroy.argtypes = [ctypes.c_void_p]
     _lib = lib
     return lib
 

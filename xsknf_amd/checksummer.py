@@ -241,3 +241,72 @@ class Checksummer:
                                    verdicts.data_ptr(), ingress_ifindex, stream.cuda_stream,
                                    frame_len_hint)
         return verdicts
+
+
+class HostPath:
+    """The batch hook with the UMEM in host memory (include/xsknf_gpu.h
+    xsknf_gpu_ctx_*): what an AF_XDP worker (src/xsknf.c:716-742) holds to run
+    its per-frame loop (:654-672) on the GPU.  `umem` is a host numpy uint8
+    array (the worker's mmap), pinned while registered; `process_batch` takes
+    host descriptors (DESC_DTYPE) and returns host int32 verdicts, with the check
+    bytes rewritten in `umem`.  path: "zerocopy" or "staged"."""
+
+    PATHS = {"zerocopy": _lib.PATH_ZEROCOPY, "staged": _lib.PATH_STAGED}
+
+    def __init__(self, checksummer: Checksummer, umem, *, path: str = "zerocopy",
+                 max_batch: int = 1 << 20, device: int = 0):
+        import numpy as np
+
+        if umem.dtype != np.uint8 or not umem.flags.c_contiguous:
+            raise ValueError("umem must be a contiguous uint8 numpy array")
+        self.cs = checksummer
+        self.umem = umem
+        self.max_batch = int(max_batch)
+        self._lib = _lib.load()
+        self._ctx = ctypes.c_void_p()
+        _lib.check(self._lib.xsknf_gpu_ctx_create(ctypes.byref(self._ctx), device, self.PATHS[path],
+                                                  self.max_batch, checksummer.frame_len_hint),
+                   "xsknf_gpu_ctx_create")
+        try:
+            _lib.check(self._lib.xsknf_gpu_ctx_register_umem(self._ctx, umem.ctypes.data, umem.nbytes),
+                       "xsknf_gpu_ctx_register_umem")
+        except Exception:
+            self.close()
+            raise
+
+    def process_batch(self, descs, ingress_ifindex: int = 0, verdicts=None):
+        import numpy as np
+
+        if descs.dtype.itemsize != 16 or not descs.flags.c_contiguous:
+            raise ValueError("descs must be a contiguous array of 16-byte xdp_desc")
+        n = int(descs.shape[0])
+        if verdicts is None:
+            verdicts = np.empty(n, dtype=np.int32)
+        opts = self.cs.csum_opts()
+        _lib.check(self._lib.xsknf_gpu_ctx_process_batch(self._ctx, descs.ctypes.data, n,
+                                                         ingress_ifindex, ctypes.byref(opts),
+                                                         verdicts.ctypes.data),
+                   "xsknf_gpu_ctx_process_batch")
+        return verdicts
+
+    def stats(self) -> dict:
+        st = _lib.CtxStats()
+        _lib.check(self._lib.xsknf_gpu_ctx_get_stats(self._ctx, ctypes.byref(st)), "xsknf_gpu_ctx_get_stats")
+        return {k: int(getattr(st, k)) for k, _ in st._fields_}
+
+    def close(self):
+        if self._ctx:
+            self._lib.xsknf_gpu_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -41,6 +41,7 @@
 #include <string.h>
 
 #include "../../include/xsknf_gpu.h"
+#include "checksummer_internal.h"
 
 namespace xsknf_gpu {
 
@@ -162,24 +163,12 @@ __device__ __forceinline__ uint32_t group_sum_last(uint32_t v) {
 
 // ---- kernel arguments, frame references, descriptors -----------------------
 
-struct KernelArgs {
-  uint8_t *umem;
-  uint64_t umem_size;
-  const xsknf_gpu_desc *descs;
-  int32_t *verdicts;
-  uint32_t n;
-  uint32_t payload_mult;   // max(csum_iterations, 0)
-  int32_t fwd_verdict;     // REDIRECT ? (ingress+1) % n_if : -1
-  uint32_t defer_min_len;  // frames at least this long park a check record for the
-                           // scatter pass; shorter ones write their check in-line
-  const uint4 *dummy;      // readable 16-byte block for frames that need no bytes
-};
+// struct KernelArgs: checksummer_internal.h
 
 // Check record parked in verdicts[f] by the summing pass (two-phase stores):
 // tag 01 in bits 31..30 (no verdict, -1 or 0..XSKNF_MAX_INTERFACES-1, has it),
 // u in bits 22..16, the new check in bits 15..0.
-constexpr uint32_t kRecTag = 0x40000000u;
-constexpr uint32_t kRecTagMask = 0xC0000000u;
+// kRecTag / kRecTagMask: checksummer_internal.h
 
 // Where a frame's bytes are and which 16-byte chunks cover them.  Frames that
 // need no bytes (len < 14, or a descriptor outside the UMEM) point at a dummy
@@ -285,7 +274,7 @@ __device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const Frame
 // run at the end of the tile, when no prefetch buffer is live (keeping them in
 // the step would cost ~60 VGPRs of occupancy for a rare case).
 constexpr uint32_t kPendTag = 0x80000000u;
-constexpr uint32_t kNoDefer = 0xffffffffu;     // defer_min_len: every check in-line
+// kNoDefer (defer_min_len: every check in-line): checksummer_internal.h
 constexpr uint32_t kDeferMinLen = 1024;        // hybrid default (tools/tune.py: 64 B, 570 B
                                                // and IMIX prefer in-line, 1500 B deferred)
 
@@ -632,6 +621,8 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
 
 thread_local char g_last_error[256] = "";
 
+void set_error_text(const char *text) { snprintf(g_last_error, sizeof(g_last_error), "%s", text); }
+
 void set_error(hipError_t e, const char *where) {
   snprintf(g_last_error, sizeof(g_last_error), "%s: %s", where, hipGetErrorString(e));
 }
@@ -679,7 +670,7 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
 
 int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess && a.defer_min_len != kNoDefer) {
+  if (e == hipSuccess && a.defer_min_len != kNoDefer && !a.no_scatter) {
     const uint32_t need = (4 * a.n + kBlock - 1) / kBlock;
     const uint32_t cap = static_cast<uint32_t>(device_cus() * 8);
     hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
@@ -762,6 +753,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
                       ? static_cast<int32_t>((ingress_ifindex + 1u) % opts->num_interfaces)
                       : -1;
   a.defer_min_len = kDeferMinLen;
+  a.no_scatter = 0;
   // aligned-down descriptor address: inside the descriptor array's own page
   a.dummy = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(descs) & ~static_cast<uintptr_t>(15));
   return 0;

@@ -1,0 +1,43 @@
+// checksummer_internal.h -- declarations shared by the gfx950 checksummer
+// kernels (checksummer.hip) and the host-path context (host_path.hip).
+// Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/xsknf_gpu.h"
+
+namespace xsknf_gpu {
+
+struct KernelArgs {
+  uint8_t *umem;
+  uint64_t umem_size;
+  const xsknf_gpu_desc *descs;
+  int32_t *verdicts;
+  uint32_t n;
+  uint32_t payload_mult;   // max(csum_iterations, 0)
+  int32_t fwd_verdict;     // REDIRECT ? (ingress+1) % n_if : -1
+  uint32_t defer_min_len;  // frames at least this long park a check record for the
+                           // scatter pass; shorter ones write their check in-line
+  const uint4 *dummy;      // readable 16-byte block for frames that need no bytes
+  uint32_t no_scatter;     // 1: leave deferred check records in `verdicts` (the host
+                           // path applies them itself)
+};
+
+// Check record parked in verdicts[f] by the summing pass (deferred stores):
+// tag 01 in bits 31..30 (no verdict, -1 or 0..XSKNF_MAX_INTERFACES-1, has it),
+// u in bits 22..16, the new check in bits 15..0.
+constexpr uint32_t kRecTag = 0x40000000u;
+constexpr uint32_t kRecTagMask = 0xC0000000u;
+constexpr uint32_t kNoDefer = 0xffffffffu;   // defer_min_len: every check in-line
+
+// Validate arguments and fill `a` (returns 1 for an empty batch, <0 on error).
+int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_desc *descs, uint32_t n,
+            uint32_t ingress_ifindex, const xsknf_csum_opts *opts, int32_t *verdicts);
+// Launch the shape `cfg` (summing kernel + scatter pass unless a.no_scatter).
+int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream);
+void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c);
+void set_error(hipError_t e, const char *where);
+void set_error_text(const char *text);
+
+}  // namespace xsknf_gpu

@@ -1,0 +1,207 @@
+// host_path.hip -- the batch hook with the UMEM in host memory.
+//
+// In the reference, an AF_XDP worker (src/xsknf.c:716-742) peeks up to
+// batch_size rx descriptors and calls xsknf_packet_processor() on each frame,
+// in place in the worker's mmap'd UMEM (src/xsknf.c:654-672, :958/:975).  This
+// context is what such a worker holds to run that loop on the GPU instead:
+// host UMEM registered once, then one synchronous call per rx batch with the
+// descriptors and verdicts in host arrays.
+//
+// ZEROCOPY: the UMEM is pinned and mapped into the device address space; the
+//   kernel reads the frames and writes the check bytes over PCIe, in place.
+//   Checks are written in-line (fused stores): a deferred sector rewrite would
+//   re-read sectors over PCIe.
+// STAGED: the byte span of the batch's frames is copied to a device mirror of
+//   the UMEM (hipMemcpyAsync from pinned memory), summed in HBM with every
+//   check deferred, and only the 4-byte per-frame records come back; the host
+//   then writes each frame's 2 check bytes itself.  Copying the span back
+//   instead would overwrite frames outside the batch that the kernel / NIC may
+//   be filling concurrently (fill-ring frames), so it never does.
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <new>
+
+#include "../../include/xsknf_gpu.h"
+#include "checksummer_internal.h"
+
+struct xsknf_gpu_ctx {
+  int device = 0;
+  int path = XSKNF_GPU_PATH_ZEROCOPY;
+  uint32_t max_batch = 0;
+  uint32_t hint = 0;
+  hipStream_t stream = nullptr;
+  uint8_t *umem_host = nullptr;
+  uint64_t umem_size = 0;
+  uint8_t *umem_dev = nullptr;        // mapped host pointer (ZEROCOPY) or device mirror (STAGED)
+  bool registered = false;
+  xsknf_gpu_desc *descs_dev = nullptr;
+  int32_t *verdicts_dev = nullptr;
+  xsknf_gpu_desc *descs_pinned = nullptr;
+  int32_t *verdicts_pinned = nullptr;
+  xsknf_gpu_ctx_stats stats = {};
+};
+
+namespace {
+
+int fail(hipError_t e, const char *where) {
+  xsknf_gpu::set_error(e, where);
+  return -EIO;
+}
+
+uint64_t umem_offset(uint64_t addr) {
+  return (addr & XSKNF_GPU_UNALIGNED_BUF_ADDR_MASK) + (addr >> XSKNF_GPU_UNALIGNED_BUF_OFFSET_SHIFT);
+}
+
+void release(xsknf_gpu_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->registered) (void)hipHostUnregister(c->umem_host);
+  if (c->path == XSKNF_GPU_PATH_STAGED && c->umem_dev) (void)hipFree(c->umem_dev);
+  if (c->descs_dev) (void)hipFree(c->descs_dev);
+  if (c->verdicts_dev) (void)hipFree(c->verdicts_dev);
+  if (c->descs_pinned) (void)hipHostFree(c->descs_pinned);
+  if (c->verdicts_pinned) (void)hipHostFree(c->verdicts_pinned);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+}  // namespace
+
+extern "C" {
+
+int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint32_t max_batch,
+                         uint32_t frame_len_hint) {
+  if (!out || max_batch == 0) return -EINVAL;
+  if (path != XSKNF_GPU_PATH_ZEROCOPY && path != XSKNF_GPU_PATH_STAGED) return -EINVAL;
+  *out = nullptr;
+  xsknf_gpu_ctx *c = new (std::nothrow) xsknf_gpu_ctx;
+  if (!c) return -ENOMEM;
+  c->device = device;
+  c->path = path;
+  c->max_batch = max_batch;
+  c->hint = frame_len_hint;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&c->descs_dev, sizeof(xsknf_gpu_desc) * max_batch);
+  if (e == hipSuccess) e = hipMalloc(&c->verdicts_dev, sizeof(int32_t) * max_batch);
+  if (e == hipSuccess) e = hipHostMalloc(&c->descs_pinned, sizeof(xsknf_gpu_desc) * max_batch, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc(&c->verdicts_pinned, sizeof(int32_t) * max_batch, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    const int rc = fail(e, "xsknf_gpu_ctx_create");
+    release(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
+}
+
+int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *c, void *umem, uint64_t size) {
+  if (!c || !umem || size == 0 || c->registered) return -EINVAL;
+  hipError_t e = hipSetDevice(c->device);
+  const unsigned flags = c->path == XSKNF_GPU_PATH_ZEROCOPY ? hipHostRegisterMapped : hipHostRegisterDefault;
+  if (e == hipSuccess) e = hipHostRegister(umem, size, flags);
+  if (e != hipSuccess) return fail(e, "hipHostRegister(umem)");
+  c->registered = true;
+  c->umem_host = static_cast<uint8_t *>(umem);
+  c->umem_size = size;
+  if (c->path == XSKNF_GPU_PATH_ZEROCOPY) {
+    void *dp = nullptr;
+    e = hipHostGetDevicePointer(&dp, umem, 0);
+    c->umem_dev = static_cast<uint8_t *>(dp);
+  } else {
+    e = hipMalloc(&c->umem_dev, size);
+  }
+  if (e != hipSuccess) {
+    (void)hipHostUnregister(umem);
+    c->registered = false;
+    c->umem_dev = nullptr;
+    return fail(e, "xsknf_gpu_ctx_register_umem");
+  }
+  return 0;
+}
+
+int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *c, const struct xsknf_gpu_desc *descs, uint32_t n,
+                                uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+                                int32_t *verdicts) {
+  using namespace xsknf_gpu;
+  if (!c || !c->registered || n > c->max_batch) return -EINVAL;
+  if (n == 0) return 0;
+  if (!descs || !verdicts) return -EINVAL;
+  KernelArgs a;
+  int rc = prepare(a, c->umem_dev, c->umem_size, c->descs_dev, n, ingress_ifindex, opts, c->verdicts_dev);
+  if (rc != 0) return rc < 0 ? rc : 0;
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return fail(e, "hipSetDevice");
+
+  memcpy(c->descs_pinned, descs, sizeof(xsknf_gpu_desc) * n);
+  e = hipMemcpyAsync(c->descs_dev, c->descs_pinned, sizeof(xsknf_gpu_desc) * n, hipMemcpyHostToDevice,
+                     c->stream);
+  if (e != hipSuccess) return fail(e, "hipMemcpyAsync(descs)");
+  c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
+
+  xsknf_gpu_launch_cfg cfg;
+  default_cfg(c->hint ? c->hint : 2048u, cfg);
+  if (c->path == XSKNF_GPU_PATH_STAGED) {
+    // byte span of the batch's (in-range) frames
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint64_t off = umem_offset(descs[i].addr);
+      if (off > c->umem_size || descs[i].len > c->umem_size - off) continue;
+      lo = off < lo ? off : lo;
+      hi = off + descs[i].len > hi ? off + descs[i].len : hi;
+    }
+    if (hi > lo) {
+      e = hipMemcpyAsync(c->umem_dev + lo, c->umem_host + lo, hi - lo, hipMemcpyHostToDevice, c->stream);
+      if (e != hipSuccess) return fail(e, "hipMemcpyAsync(umem span)");
+      c->stats.bytes_h2d += hi - lo;
+    }
+    cfg.fused_stores = 2;   // every check deferred ...
+    a.no_scatter = 1;       // ... and applied on the host below
+  } else {
+    cfg.fused_stores = 1;   // in place over PCIe
+  }
+  rc = run(a, cfg, c->stream);
+  if (rc != 0) return rc;
+  e = hipMemcpyAsync(c->verdicts_pinned, c->verdicts_dev, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return fail(e, "verdict copy-back");
+  c->stats.bytes_d2h += sizeof(int32_t) * n;
+
+  if (c->path == XSKNF_GPU_PATH_STAGED) {
+    // checksummer_user.c:108 on the host: the 2 check bytes of every summed frame
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t r = static_cast<uint32_t>(c->verdicts_pinned[i]);
+      if ((r & kRecTagMask) == kRecTag) {
+        uint8_t *p = c->umem_host + umem_offset(descs[i].addr) + ((r >> 16) & 0x7f) + 6;
+        p[0] = static_cast<uint8_t>(r);
+        p[1] = static_cast<uint8_t>(r >> 8);
+        verdicts[i] = a.fwd_verdict;
+      } else {
+        verdicts[i] = static_cast<int32_t>(r);
+      }
+    }
+  } else {
+    memcpy(verdicts, c->verdicts_pinned, sizeof(int32_t) * n);
+  }
+  c->stats.batches += 1;
+  c->stats.frames += n;
+  return 0;
+}
+
+int xsknf_gpu_ctx_get_stats(const struct xsknf_gpu_ctx *c, struct xsknf_gpu_ctx_stats *stats) {
+  if (!c || !stats) return -EINVAL;
+  *stats = c->stats;
+  return 0;
+}
+
+int xsknf_gpu_ctx_destroy(struct xsknf_gpu_ctx *c) {
+  if (!c) return -EINVAL;
+  release(c);
+  return 0;
+}
+
+}  // extern "C"
