@@ -1,0 +1,63 @@
+"""Multi-rank path on CPU (gloo, world size 2): byte-balanced contiguous shards
+that partition the batch, per-rank checksumming by the oracle on each shard, and
+the counter all-reduce bench.py does on RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from xsknf_amd import frames
+from xsknf_amd.shard import allreduce_counters, counters, shard_by_bytes
+
+
+def test_shard_by_bytes_partitions_and_balances():
+    rng = np.random.default_rng(3)
+    lens = frames.imix_lengths(1 << 16, rng)
+    for world in (1, 2, 3, 4, 8):
+        r = shard_by_bytes(lens, world)
+        assert r[0][0] == 0 and r[-1][1] == lens.shape[0]
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        sums = [int(lens[lo:hi].sum()) for lo, hi in r]
+        assert max(sums) - min(sums) <= 2 * 1500
+    assert shard_by_bytes(np.zeros(0), 4) == [(0, 0)] * 4
+    assert shard_by_bytes(np.array([1500]), 3)[-1][1] == 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import csum_oracle as O
+    b = frames.aligned_batch(2000, "imix", seed=11)
+    lo, hi = shard_by_bytes(b.descs["len"], world)[rank]
+    sub = frames.HostBatch(b.umem.copy(), np.ascontiguousarray(b.descs[lo:hi]), b.layout)
+    v = O.c_process_batch(sub.umem, sub.descs)
+    c = allreduce_counters(dist, counters(v, sub.descs["len"]))
+    out[rank] = (lo, hi, c.tolist())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_shards_and_counters():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    b = frames.aligned_batch(2000, "imix", seed=11)
+    ranges = sorted((out[r][0], out[r][1]) for r in range(world))
+    assert ranges[0][0] == 0 and ranges[-1][1] == b.n and ranges[0][1] == ranges[1][0]
+    total = out[0][2]
+    assert total == out[1][2]
+    assert total[0] == b.n and total[1] == int(b.descs["len"].astype(np.int64).sum())
+    assert total[2] + total[3] == b.n
