@@ -6,11 +6,36 @@ LIBDIR := xsknf_amd/lib
 LIB := $(LIBDIR)/libxsknf_gpu.so
 SRCS := xsknf_amd/csrc/checksummer.hip xsknf_amd/csrc/host_path.hip
 
-all: $(LIB) oracle
+# host side: the AF_XDP runtime (plain C) and the checksummer NF binary
+CC ?= gcc
+CFLAGS ?= -O2 -g -std=gnu11 -Wall -Wextra -fPIC -fvisibility=hidden -Iinclude
+RTLIB := $(LIBDIR)/libxsknf.so
+RTSRCS := xsknf_amd/csrc/xsknf_rt.c xsknf_amd/csrc/rt_netlink.c
+RTHDRS := include/xsknf.h xsknf_amd/csrc/xsk_ring.h xsknf_amd/csrc/rt_netlink.h
+APP := xsknf_amd/bin/checksummer
+
+all: $(LIB) $(RTLIB) $(APP) oracle
 
 $(LIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h Makefile
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+
+$(RTLIB): $(RTSRCS) $(RTHDRS) Makefile
+	@mkdir -p $(LIBDIR)
+	$(CC) $(CFLAGS) -shared -pthread -o $@ $(RTSRCS)
+
+$(APP): xsknf_amd/csrc/checksummer_app.c $(RTLIB) $(LIB) include/xsknf.h include/xsknf_gpu.h
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -o $@ $< -L$(LIBDIR) -lxsknf -lxsknf_gpu -Wl,-rpath,'$$ORIGIN/../lib' -pthread
+
+# config-1 harness (test / measurement infra: links the CPU oracle as the NF)
+VETH := tools/build/xsk_veth
+tools: $(VETH)
+$(VETH): tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c $(RTLIB) oracle
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c \
+		-L$(LIBDIR) -lxsknf -Loracle/build -lcsum_oracle \
+		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread
 
 # keep the device assembly for inspection (VGPRs, instruction mix)
 asm: $(SRCS)
@@ -21,7 +46,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(LIBDIR) build
+	rm -rf $(LIBDIR) xsknf_amd/bin build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean
+.PHONY: all oracle asm clean tools

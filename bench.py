@@ -53,6 +53,10 @@ def parse():
                    help="comma list of extra workloads timed after the primary ('' = none)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
+    p.add_argument("--cpu-all-cores", type=int, default=-1,
+                   help="threads for the all-cores CPU leg (-1 = the process's CPUs, at most 16; 0 = skip)")
+    p.add_argument("--kernel-steps", type=int, default=50,
+                   help="launches of the summing kernel alone for the roofline (0 = skip)")
     return p.parse_args()
 
 
@@ -128,16 +132,51 @@ def time_workload(name, args, world, rank, dev, seed):
     kernel_ms = ev0.elapsed_time(ev1) / args.steps       # HIP events on the launch stream
     wall_max = allreduce_max(wall, world)
 
+    # dominant kernel alone: the summing kernel in records-only mode
+    # (include/xsknf_gpu.h fused_stores = 3), same shape, same stream, HIP
+    # events around K launches.  It only reads the UMEM, so the step's output
+    # is unaffected; for frames >= 1024 B (every frame of 1500 / jumbo) it is
+    # exactly the step's first kernel, which defers every check there too.
+    k_ms = None
+    if args.kernel_steps > 0:
+        import ctypes
+        from xsknf_amd import _lib
+        lib = _lib.load()
+        cfg = _lib.LaunchCfg()
+        _lib.check(lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(cfg)), "default_launch_cfg")
+        cfg.fused_stores = 3
+        rec = torch.empty(n, dtype=torch.int32, device=dev)
+        opts = cs.csum_opts()
+
+        def kstep():
+            rc = lib.xsknf_gpu_checksum_batch_cfg(
+                ctypes.c_void_p(umem_ptr), umem.numel(), ctypes.c_void_p(descs_ptr), n, 0, ctypes.byref(opts),
+                ctypes.c_void_p(rec.data_ptr()), ctypes.byref(cfg), ctypes.c_void_p(stream.cuda_stream))
+            _lib.check(rc, "records-only launch")
+
+        for _ in range(3):
+            kstep()
+        barrier(world)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.kernel_steps):
+            kstep()
+        e1.record(stream)
+        barrier(world)
+        k_ms = e0.elapsed_time(e1) / args.kernel_steps
+        del rec
+
     vh = verdicts.cpu().numpy()
     bytes_len = int(lens.sum())
     counters = allreduce_sum_i64([n, bytes_len, int((vh == -1).sum()), int((vh >= 0).sum())], world)
-    res = dict(name=name, desc=desc, n=n, lens=lens, bytes_len=bytes_len, kernel_ms=kernel_ms,
+    res = dict(name=name, desc=desc, n=n, lens=lens, bytes_len=bytes_len, kernel_ms=kernel_ms, sum_ms=k_ms,
                wall_max=wall_max, counters=counters, umem=umem, descs=descs, verdicts=verdicts,
                sample=sample, layout=layout, chunk=chunk)
     return res
 
 
-def cpu_baseline(res, budget_s, threads):
+def cpu_baseline(res, budget_s, threads, check=True):
     """Oracle (the C restatement, gcc -O2 -flto) timed on host cores over a bounded
     sample of the same workload; also checks the GPU result on that sample."""
     from oracle import csum_oracle as O
@@ -151,11 +190,13 @@ def cpu_baseline(res, budget_s, threads):
     gbs = lens.sum() * reps / t / 1e9
     # checker: GPU output on the sample frames == oracle output (single pass;
     # reprocessing is idempotent because the check is cleared before summing)
-    O.c_process_batch(umem_host, descs_host)
-    hi = umem_host.shape[0]
-    g_umem = res["umem"][:hi].cpu().numpy()
-    g_v = res["verdicts"][:k].cpu().numpy()
-    match = bool(np.array_equal(g_v, v) and np.array_equal(g_umem, umem_host))
+    match = None
+    if check:
+        O.c_process_batch(umem_host, descs_host)
+        hi = umem_host.shape[0]
+        g_umem = res["umem"][:hi].cpu().numpy()
+        g_v = res["verdicts"][:k].cpu().numpy()
+        match = bool(np.array_equal(g_v, v) and np.array_equal(g_umem, umem_host))
     return {"value": round(float(gbs), 4), "unit": "GB/s checksummed", "cores": threads,
             "kind": "port", "mpps": round(k * reps / t / 1e6, 4),
             "sample": f"{k} frames of the same workload ({lens.sum() / 1e6:.1f} MB) x {reps} passes, "
@@ -168,7 +209,10 @@ def traffic_for(name):
     p = os.path.join(ROOT, "profiles", f"traffic_{name}.json")
     if os.path.exists(p):
         try:
-            return json.load(open(p)).get("hbm_bytes_per_launch")
+            d = json.load(open(p))
+            # the dominant kernel's bytes per launch (tools/traffic.py); rocprof PMC
+            # passes of an earlier run, committed under profiles/
+            return (d.get("dominant") or {}).get("hbm_bytes_per_launch")
         except Exception:
             return None
     return None
@@ -186,23 +230,42 @@ def main():
         total_frames, total_bytes = r["counters"][0], r["counters"][1]
         sec[name] = {"mpps": round(total_frames / (r["wall_max"] / args.steps) / 1e6, 2),
                      "gbs_checksummed": round(total_bytes / (r["wall_max"] / args.steps) / 1e9, 2),
-                     "kernel_us": round(r["kernel_ms"] * 1e3, 2)}
+                     "step_us": round(r["kernel_ms"] * 1e3, 2),
+                     "sum_kernel_us": round(r["sum_ms"] * 1e3, 2) if r["sum_ms"] else None}
         del r
 
     total_frames, total_bytes, n_drop, n_fwd = prim["counters"]
     step_s = prim["wall_max"] / args.steps
     value = total_bytes / step_s / 1e9
     mpps = total_frames / step_s / 1e6
-    # roofline of the dominant (only) kernel, per launch on this rank
-    k_s = prim["kernel_ms"] / 1e3
-    alg_bytes = prim["bytes_len"] + prim["n"] * (DESC_BYTES + VERDICT_BYTES + CHECK_BYTES)
+    # roofline of the dominant kernel (the summing kernel), per launch on this
+    # rank: algorithmic bytes = every frame byte + its 16 B descriptor read +
+    # its 4 B record / verdict write (SURVEY.md 8(d) minus the 2 B check, which
+    # the scatter kernel writes) over its average duration from HIP events
+    step_k_s = prim["kernel_ms"] / 1e3
+    step_alg = prim["bytes_len"] + prim["n"] * (DESC_BYTES + VERDICT_BYTES + CHECK_BYTES)
+    if prim["sum_ms"] is not None:
+        k_s = prim["sum_ms"] / 1e3
+        alg_bytes = prim["bytes_len"] + prim["n"] * (DESC_BYTES + VERDICT_BYTES)
+        kernel = "checksum_kernel (records only, launched alone)"
+    else:
+        k_s, alg_bytes, kernel = step_k_s, step_alg, "whole step"
     achieved = alg_bytes / k_s / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_for(args.workload),
-            "alg_bytes_per_launch": alg_bytes, "kernel_us": round(prim["kernel_ms"] * 1e3, 2)}
+            "kernel": kernel, "alg_bytes_per_launch": alg_bytes, "kernel_us": round(k_s * 1e6, 2),
+            # SURVEY.md 8(d)'s whole-step figure: sum(len + 22) / step time (both kernels)
+            "step_us": round(step_k_s * 1e6, 2), "step_alg_bytes": step_alg,
+            "step_frac": round(step_alg / step_k_s / 1e9 / HBM_PEAK_GBS, 4)}
     cpu = None
     if rank == 0 and prim["sample"] is not None:
         cpu = cpu_baseline(prim, args.cpu_seconds, args.cpu_threads)
+        n_all = args.cpu_all_cores
+        if n_all < 0:
+            n_all = min(16, len(os.sched_getaffinity(0)))
+        if n_all > 1:
+            allc = cpu_baseline(prim, args.cpu_seconds / 2, n_all, check=False)
+            cpu["all_cores"] = {k: allc[k] for k in ("value", "unit", "cores", "mpps", "sample")}
     if rank == 0:
         length, layout, chunk, desc = WORKLOADS[args.workload]
         out = {

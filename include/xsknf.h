@@ -1,0 +1,155 @@
+/* xsknf.h -- AF_XDP network-function runtime with a GPU batch hook.
+ *
+ * Source-compatible with the reference's library surface (src/xsknf.h:1-75):
+ * same function names, `struct xsknf_config` / `struct xsknf_socket_stats`
+ * with the same members in the same order, MODE_* and XSKNF_MAX_*.  An NF
+ * written against the reference (examples/checksummer/checksummer_user.c)
+ * links against libxsknf.so unchanged.
+ *
+ * Built on raw linux/if_xdp.h (sockets, XDP_UMEM_REG, ring mmaps) with a
+ * built-in XSKMAP-redirect XDP program; libxdp/libbpf are not used.
+ *
+ * Differences from the reference, each deliberate:
+ *  - errors after argument parsing are returned as -errno instead of
+ *    exit(EXIT_FAILURE) (src/xsknf.c:108-119); xsknf_parse_args() still
+ *    prints the usage and exits on bad arguments, like the reference;
+ *  - MODE_XDP / MODE_COMBINED (loading the NF's own <app>_kern.o through
+ *    libbpf, src/xsknf.c:357-392) return -EOPNOTSUPP from xsknf_init();
+ *  - the ring-level stats are filled (the reference passes
+ *    optlen = sizeof(pointer) to XDP_STATISTICS, src/xsknf.c:90, so the
+ *    kernel rejects it and they stay 0);
+ *  - batches are not limited to 255 frames (uint8 counters, src/xsknf.c:633);
+ *  - multi-interface recycling and cross-UMEM copies translate unaligned
+ *    addresses first (src/xsknf.c:449 and :551 use the raw address);
+ *  - a verdict >= num_interfaces is dropped instead of indexing past
+ *    to_tx[] (src/xsknf.c:519).
+ *
+ * Additions (not in the reference): xsknf_set_packet_processor(),
+ * xsknf_set_batch_processor() -- the GPU hook -- xsknf_get_umem(),
+ * xsknf_worker_error(), and emulated queues (interface names "emu<k>")
+ * whose kernel side is driven by xsknf_emu_deliver() / xsknf_emu_transmit().
+ */
+#ifndef XSKNF_AMD_XSKNF_H
+#define XSKNF_AMD_XSKNF_H
+
+#include <stdint.h>
+#include <linux/if_xdp.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef XSKNF_API
+#define XSKNF_API __attribute__((visibility("default")))
+#endif
+
+#define XSKNF_MAX_INTERFACES 32
+#define XSKNF_MAX_WORKERS 32
+
+/* Application working modes (src/xsknf.h:15-17) */
+#define MODE_AF_XDP 0x1
+#define MODE_XDP 0x2
+#define MODE_COMBINED (MODE_AF_XDP | MODE_XDP)
+
+/* Opaque: kept so xsknf_init() has the reference's signature (src/xsknf.h:63). */
+struct bpf_object;
+
+/* Per-frame NF callback (src/xsknf.h:19-23): returns the interface index to
+ * redirect the frame to, or -1 to drop it.  A link-time symbol, like in the
+ * reference; xsknf_set_packet_processor() overrides it. */
+int xsknf_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex);
+
+struct xsknf_config {                       /* src/xsknf.h:25-40 */
+	char *interfaces[XSKNF_MAX_INTERFACES];
+	uint32_t bind_flags[XSKNF_MAX_INTERFACES];
+	unsigned num_interfaces;
+	unsigned workers;
+	unsigned working_mode;
+	uint32_t xdp_flags;
+	uint32_t batch_size;
+	int poll;
+	int unaligned_chunks;
+	int xsk_frame_size;
+	int busy_poll;
+	char ebpf_filename[256];
+	char xdp_progname[256];
+	char tc_progname[256];
+};
+
+struct xsknf_socket_stats {                 /* src/xsknf.h:42-59, 13 counters */
+	/* Ring level stats */
+	unsigned long rx_npkts;
+	unsigned long tx_npkts;
+	unsigned long rx_dropped_npkts;
+	unsigned long rx_invalid_npkts;
+	unsigned long tx_invalid_npkts;
+	unsigned long rx_full_npkts;
+	unsigned long rx_fill_empty_npkts;
+	unsigned long tx_empty_npkts;
+
+	/* Application level stats */
+	unsigned long rx_empty_polls;
+	unsigned long fill_fail_polls;
+	unsigned long tx_wakeup_sendtos;
+	unsigned long tx_trigger_sendtos;
+	unsigned long opt_polls;
+};
+
+/* src/xsknf.h:62-68 */
+XSKNF_API int xsknf_parse_args(int argc, char **argv, struct xsknf_config *config);
+XSKNF_API int xsknf_init(struct xsknf_config *config, struct bpf_object **bpf_obj);
+XSKNF_API int xsknf_cleanup(void);
+XSKNF_API int xsknf_start_workers(void);
+XSKNF_API int xsknf_stop_workers(void);
+XSKNF_API int xsknf_get_socket_stats(unsigned worker_idx, unsigned iface_idx,
+		struct xsknf_socket_stats *stats);
+
+/* ---- additions ---------------------------------------------------------- */
+
+typedef int (*xsknf_packet_processor_fn)(void *pkt, unsigned len, unsigned ingress_ifindex);
+
+/* Batch hook, called at the position of the per-frame loop of
+ * process_batch_1if / process_batch (src/xsknf.c:654-672, :500-522) from the
+ * worker thread, once per rx batch: `descs` are the batch's rx descriptors
+ * (contiguous even when the ring wrapped), `umem` the base of the UMEM they
+ * address.  It fills verdicts[i] with the callback's meaning and returns 0,
+ * or a negative errno, which stops the worker (see xsknf_worker_error()). */
+typedef int (*xsknf_batch_processor_fn)(void *user, unsigned worker_idx, void *umem,
+		uint64_t umem_size, const struct xdp_desc *descs, uint32_t n,
+		unsigned ingress_ifindex, int32_t *verdicts);
+
+/* Select the NF: call before xsknf_start_workers().  The batch hook takes
+ * precedence; with neither set, the xsknf_packet_processor symbol is used. */
+XSKNF_API int xsknf_set_packet_processor(xsknf_packet_processor_fn fn);
+XSKNF_API int xsknf_set_batch_processor(xsknf_batch_processor_fn fn, void *user);
+
+/* The UMEM buffer a worker's socket on iface_idx uses (after xsknf_init). */
+XSKNF_API int xsknf_get_umem(unsigned worker_idx, unsigned iface_idx, void **buffer,
+		uint64_t *size);
+
+/* 0 while the worker runs cleanly, else the -errno that stopped it. */
+XSKNF_API int xsknf_worker_error(unsigned worker_idx);
+
+/* Emulated queues: an interface named "emu<k>" gets in-memory rings with the
+ * kernel's semantics instead of an AF_XDP socket, and these two calls play
+ * the kernel's part (single caller thread per queue).
+ *
+ * deliver: takes fill-ring entries and copies up to n frames (frame i at
+ *   data + i*stride, lens[i] bytes) into them at the XDP headroom, posting rx
+ *   descriptors as the kernel does (aligned: chunk+256; unaligned:
+ *   addr | 256 << 48).  Returns the number delivered; stops early when the
+ *   fill ring is empty or the rx ring full.  -EINVAL for a frame that does
+ *   not fit a chunk.
+ * transmit: consumes up to max tx descriptors, copies each frame to
+ *   out + i*stride (lens[i] = its length, truncated to stride) and returns
+ *   its address on the completion ring.  Returns the number consumed. */
+XSKNF_API int xsknf_emu_deliver(unsigned worker_idx, unsigned iface_idx, const uint8_t *data,
+		const uint32_t *lens, uint32_t n, uint32_t stride);
+XSKNF_API int xsknf_emu_transmit(unsigned worker_idx, unsigned iface_idx, uint8_t *out,
+		uint32_t *lens, uint32_t max, uint32_t stride);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* XSKNF_AMD_XSKNF_H */

@@ -97,12 +97,22 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * slots (frames_per_group is then ignored); 0 selects the register kernel.
  * `fused_stores` = 1 writes every check from the summing kernel itself; 2 parks
  * every check for a second, write-only pass (non-temporal full 64-byte sector
- * rewrites); 0 (default) decides per frame: frames of 256 bytes or more are
+ * rewrites); 0 (default) decides per frame: frames of 1024 bytes or more are
  * deferred (scattered writes mixed into the read stream cost ~25 % of its
  * bandwidth on MI355X), shorter ones write in-line (their check shares the line
- * just read).  Only instantiated shapes are accepted (-EINVAL
+ * just read).  3 = records only: the summing kernel runs alone, the UMEM is
+ * only read, and every summed frame's verdicts[i] is left as the record
+ *   XSKNF_GPU_RECORD_TAG | (u << 16) | check,   u = bits 22..16,
+ * meaning "write the 16-bit `check` (as stored in memory, low byte first) at
+ * frame offset u + 6, verdict = the forward verdict"; frames that are not
+ * summed carry their final verdict.  The STAGED host path uses this mode (the
+ * host applies the checks); benchmarks use it to time the summing kernel.
+ * Only instantiated shapes are accepted (-EINVAL
  * otherwise); every shape gives identical results.
  */
+#define XSKNF_GPU_RECORD_TAG 0x40000000u       /* bits 31..30 = 01 */
+#define XSKNF_GPU_RECORD_TAG_MASK 0xC0000000u
+
 struct xsknf_gpu_launch_cfg {
 	int32_t lanes_per_frame;
 	int32_t chunks_per_lane;
@@ -131,8 +141,9 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            the frames and writes the check bytes in place
  *                            over PCIe (no copies).
  *   XSKNF_GPU_PATH_STAGED    the byte span of each batch is copied to a device
- *                            mirror (hipMemcpyAsync from the pinned UMEM),
- *                            checksummed in HBM and copied back.
+ *                            mirror (hipMemcpyAsync from the pinned UMEM) and
+ *                            checksummed in HBM; only the 4-byte records come
+ *                            back and the host writes the 2 check bytes.
  * One context = one worker thread = one HIP stream.  Calls are synchronous:
  * when xsknf_gpu_ctx_process_batch() returns, verdicts and check bytes are in
  * host memory.
@@ -158,6 +169,26 @@ XSKNF_GPU_API int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *ctx,
 		const struct xsknf_csum_opts *opts, int32_t *verdicts);
 XSKNF_GPU_API int xsknf_gpu_ctx_get_stats(const struct xsknf_gpu_ctx *ctx, struct xsknf_gpu_ctx_stats *stats);
 XSKNF_GPU_API int xsknf_gpu_ctx_destroy(struct xsknf_gpu_ctx *ctx);
+
+/* ---- batch hook for the AF_XDP runtime (include/xsknf.h) ------------------
+ * The checksummer NF as an xsknf_batch_processor_fn: it replaces the per-frame
+ * xsknf_packet_processor() loop of process_batch_1if / process_batch
+ * (src/xsknf.c:654-672, :500-522).  Each worker gets its own context (device
+ * worker_idx % device count, `path` as above), created on the worker's first
+ * batch for each UMEM it sees, so no call crosses threads.  Register with
+ *   xsknf_set_batch_processor((xsknf_batch_processor_fn)xsknf_gpu_hook_process, hook);
+ * Stop the workers before xsknf_gpu_hook_destroy(), and destroy the hook
+ * before xsknf_cleanup() unmaps the UMEMs. */
+struct xsknf_gpu_hook;
+
+XSKNF_GPU_API int xsknf_gpu_hook_create(struct xsknf_gpu_hook **hook, const struct xsknf_csum_opts *opts,
+		uint32_t workers, int path, uint32_t max_batch, uint32_t frame_len_hint);
+XSKNF_GPU_API int xsknf_gpu_hook_process(void *hook, uint32_t worker_idx, void *umem, uint64_t umem_size,
+		const struct xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex, int32_t *verdicts);
+/* Sum of the worker's context stats. */
+XSKNF_GPU_API int xsknf_gpu_hook_get_stats(const struct xsknf_gpu_hook *hook, uint32_t worker_idx,
+		struct xsknf_gpu_ctx_stats *stats);
+XSKNF_GPU_API int xsknf_gpu_hook_destroy(struct xsknf_gpu_hook *hook);
 
 /* Text of the last HIP error seen by this library on the calling thread. */
 XSKNF_GPU_API const char *xsknf_gpu_last_error(void);

@@ -204,3 +204,22 @@ double oracle_time_batch(uint8_t *umem, const struct oracle_desc *descs,
 	clock_gettime(CLOCK_MONOTONIC, &t1);
 	return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---- the callback as the reference app links it ---------------------
+ * xsknf_packet_processor(pkt, len, ingress) with the options in globals, as
+ * checksummer_user.c:24-28 keeps them: lets the AF_XDP runtime
+ * (include/xsknf.h, xsknf_set_packet_processor) run the reference per-frame
+ * path for config 1 (checksummer over veth, CPU only) and the runtime tests. */
+static struct oracle_opts nf_opts = {1, 0, 1, 0};
+
+void oracle_nf_set_options(int32_t csum_iterations, int32_t action, uint32_t num_interfaces)
+{
+	nf_opts.csum_iterations = csum_iterations;
+	nf_opts.action = action;
+	nf_opts.num_interfaces = num_interfaces;
+}
+
+int oracle_nf_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex)
+{
+	return oracle_packet_processor(pkt, len, ingress_ifindex, &nf_opts);
+}

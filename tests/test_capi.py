@@ -15,14 +15,20 @@ from xsknf_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
+def declared_functions(header="xsknf_gpu.h", api="XSKNF_GPU_API"):
+    """Functions a header declares with its export macro (include/xsknf_gpu.h:
+    XSKNF_GPU_API -> libxsknf_gpu.so; include/xsknf.h: XSKNF_API -> libxsknf.so)."""
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     names = set()
-    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
-        src = open(h).read()
-        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        for m in re.finditer(r"\b(xsknf_gpu_\w+)\s*\(", src):
-            names.add(m.group(1))
+    for m in re.finditer(rf"\b{api}\b[^;(]*?\b(xsknf_\w+)\s*\(", src):
+        names.add(m.group(1))
     return sorted(names)
+
+
+def test_every_header_is_covered():
+    assert sorted(os.path.basename(h) for h in glob.glob(os.path.join(ROOT, "include", "*.h"))) == \
+        ["xsknf.h", "xsknf_gpu.h"]
 
 
 def test_header_declares_the_binding_list():

@@ -207,6 +207,41 @@ def test_every_launch_shape_is_bit_exact(dev, shape, layout):
     assert np.array_equal(umem.cpu().numpy(), ou)
 
 
+@pytest.mark.parametrize("shape", [(16, 2, 4, 0), (8, 1, 4, 0), (64, 4, 1, 3)], ids=["reg16", "reg8", "dma64"])
+def test_records_only_mode(dev, shape):
+    """fused_stores = 3: the UMEM is only read; applying the records as
+    include/xsknf_gpu.h documents them gives the oracle's bytes and verdicts."""
+    import ctypes
+    from xsknf_amd import _lib
+    lib = _lib.load()
+    b = frames.unaligned_batch(3000, "imix", seed=77)
+    frames.inject_edge_cases(b, 0.1)
+    ou, ov = run_oracle(b, iters=2, action=O.REDIRECT, nif=3, ingress=1)
+    umem = torch.from_numpy(b.umem).to(dev)
+    descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+    v = torch.empty(b.n, dtype=torch.int32, device=dev)
+    cfg = _lib.LaunchCfg(shape[0], shape[1], shape[2], 4, shape[3], 3)
+    assert lib.xsknf_gpu_checksum_batch_cfg(
+        ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), b.n, 1,
+        ctypes.byref(_lib.CsumOpts(2, O.REDIRECT, 3, 0)), ctypes.c_void_p(v.data_ptr()),
+        ctypes.byref(cfg), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(umem.cpu().numpy(), b.umem)          # not written
+    rec = v.cpu().numpy().view(np.uint32)
+    host = b.umem.copy()
+    verd = rec.view(np.int32).copy()
+    tagged = (rec & 0xC0000000) == 0x40000000
+    offs = b.frame_offsets()
+    for i in np.flatnonzero(tagged):
+        at = int(offs[i]) + int((rec[i] >> 16) & 0x7F) + 6
+        host[at] = rec[i] & 0xFF
+        host[at + 1] = (rec[i] >> 8) & 0xFF
+        verd[i] = (1 + 1) % 3                                    # forward verdict
+    assert tagged.sum() > b.n // 2
+    assert np.array_equal(verd, ov)
+    assert np.array_equal(host, ou)
+
+
 @pytest.mark.parametrize("path", ["zerocopy", "staged"])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
 def test_host_path_bit_exact(dev, path, layout):

@@ -183,6 +183,46 @@ __global__ __launch_bounds__(256) void scatter_coal(uint8_t *__restrict__ base, 
   }
 }
 
+// read pass: pieces of the first `head` bytes of every chunk with the default
+// (cache-allocating) policy, the rest non-temporal
+__global__ __launch_bounds__(256) void probe_head(const uint8_t *__restrict__ base, uint64_t pieces,
+                                                  uint32_t ppc, uint32_t stride, uint32_t off,
+                                                  uint32_t *__restrict__ out, uint32_t head) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  uint32_t acc = 0;
+  const uint64_t tid = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t nthr = gridDim.x * 256ull;
+  for (uint64_t i = tid; i < pieces; i += 4 * nthr) {
+    u4v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t j = min(i + k * nthr, pieces - 1);
+      const uint64_t c = j / ppc, p = j % ppc;
+      const u4v *a = reinterpret_cast<const u4v *>(base + c * stride + off + p * 16);
+      v[k] = (p * 16 < head) ? *a : __builtin_nontemporal_load(a);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// scatter with the sector re-read: 4 lanes read the 64-B sector around byte
+// off+40 (default policy) and write it back whole (nt), as the product's pass
+__global__ __launch_bounds__(256) void scatter_rw(uint8_t *__restrict__ base, uint64_t chunks,
+                                                  uint32_t stride, uint32_t off,
+                                                  const uint32_t *__restrict__ vals) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < chunks * 4; t += gridDim.x * 256ull) {
+    const uint64_t c = t / 4;
+    const int piece = t % 4;
+    uint8_t *sec = base + ((c * stride + off + 40) & ~(uint64_t)63);
+    u4v v = *reinterpret_cast<const u4v *>(sec + 16 * piece);
+    v.x ^= vals[c] & 1;
+    __builtin_nontemporal_store(v, reinterpret_cast<u4v *>(sec + 16 * piece));
+  }
+}
+
 int main(int argc, char **argv) {
   if (argc < 5) { fprintf(stderr, "usage: %s chunks stride off len [reps]\n", argv[0]); return 2; }
   const uint64_t chunks = strtoull(argv[1], 0, 0);
@@ -272,6 +312,28 @@ int main(int argc, char **argv) {
         if (r > 0) { rsum += t1; ssum += t2; }
       }
       printf("{\"seq_mode\": %d, \"read_us\": %.2f, \"scatter_us\": %.2f}\n", mode,
+             rsum * 1e3 / (reps - 1), ssum * 1e3 / (reps - 1));
+    }
+  }
+  if (getenv("PROBE_HEAD")) {
+    const uint32_t heads[] = {0, 64, 128, 256};
+    for (uint32_t hd : heads) {
+      double rsum = 0, ssum = 0;
+      for (int r = 0; r < reps; ++r) {
+        hipEvent_t a0, a1, a2;
+        CHECK(hipEventCreate(&a0)); CHECK(hipEventCreate(&a1)); CHECK(hipEventCreate(&a2));
+        CHECK(hipEventRecord(a0));
+        hipLaunchKernelGGL(probe_head, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out, hd);
+        CHECK(hipEventRecord(a1));
+        hipLaunchKernelGGL(scatter_rw, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        CHECK(hipEventRecord(a2));
+        CHECK(hipEventSynchronize(a2));
+        float t1 = 0, t2 = 0;
+        CHECK(hipEventElapsedTime(&t1, a0, a1));
+        CHECK(hipEventElapsedTime(&t2, a1, a2));
+        if (r > 0) { rsum += t1; ssum += t2; }
+      }
+      printf("{\"head\": %u, \"read_us\": %.2f, \"scatter_rw_us\": %.2f}\n", hd,
              rsum * 1e3 / (reps - 1), ssum * 1e3 / (reps - 1));
     }
   }

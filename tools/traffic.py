@@ -42,8 +42,15 @@ def main():
     # kernel); the scatter pass reads 64-B sectors and 4-16 B words, counted 1:1
     fetch_b = sum((2 if "checksum_kernel" in k else 1) * 1024 * v for k, v in fetch.items())
     write_b = sum(1024 * v for v in write.values())
+    # the dominant kernel alone (bench.py's roofline.traffic): the summing kernel
+    sk = [k for k in fetch if "checksum_kernel" in k]
+    dom = None
+    if sk:
+        k = max(sk, key=lambda k: fetch[k])
+        dom = {"kernel": k, "hbm_bytes_per_launch": int(2 * 1024 * fetch[k] + 1024 * write.get(k, 0.0))}
     out = {
         "workload": workload,
+        "dominant": dom,
         "hbm_bytes_per_launch": int(fetch_b + write_b),
         "fetch_bytes": int(fetch_b), "write_bytes": int(write_b),
         "per_kernel_fetch_KiB_raw": fetch, "per_kernel_write_KiB_raw": write,
@@ -55,5 +62,17 @@ def main():
     print(json.dumps(out, indent=1))
 
 
+def add_dominant(path):
+    """Add the `dominant` entry to an existing traffic_<workload>.json."""
+    d = json.load(open(path))
+    fetch, write = d["per_kernel_fetch_KiB_raw"], d["per_kernel_write_KiB_raw"]
+    k = max((k for k in fetch if "checksum_kernel" in k), key=lambda k: fetch[k])
+    d["dominant"] = {"kernel": k, "hbm_bytes_per_launch": int(2 * 1024 * fetch[k] + 1024 * write.get(k, 0.0))}
+    json.dump(d, open(path, "w"), indent=1)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1] == "--add-dominant":
+        add_dominant(sys.argv[2])
+    else:
+        main()

@@ -25,6 +25,10 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_ctx_process_batch",
     "xsknf_gpu_ctx_get_stats",
     "xsknf_gpu_ctx_destroy",
+    "xsknf_gpu_hook_create",
+    "xsknf_gpu_hook_process",
+    "xsknf_gpu_hook_get_stats",
+    "xsknf_gpu_hook_destroy",
 )
 
 PATH_ZEROCOPY = 0
@@ -118,6 +122,16 @@ def load() -> ctypes.CDLL:
     lib.xsknf_gpu_ctx_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(CtxStats)]
     lib.xsknf_gpu_ctx_destroy.restype = ctypes.c_int
     lib.xsknf_gpu_ctx_destroy.argtypes = [ctypes.c_void_p]
+    lib.xsknf_gpu_hook_create.restype = ctypes.c_int
+    lib.xsknf_gpu_hook_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(CsumOpts),
+                                          ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32]
+    lib.xsknf_gpu_hook_process.restype = ctypes.c_int
+    lib.xsknf_gpu_hook_process.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    lib.xsknf_gpu_hook_get_stats.restype = ctypes.c_int
+    lib.xsknf_gpu_hook_get_stats.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(CtxStats)]
+    lib.xsknf_gpu_hook_destroy.restype = ctypes.c_int
+    lib.xsknf_gpu_hook_destroy.argtypes = [ctypes.c_void_p]
     _lib = lib
     return lib
 

@@ -761,11 +761,12 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
 
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
-  if (cfg.fused_stores < 0 || cfg.fused_stores > 2) return -EINVAL;
+  if (cfg.fused_stores < 0 || cfg.fused_stores > 3) return -EINVAL;
   const Variant *v = find_variant(cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group, cfg.lds_ring);
   if (!v) return -EINVAL;
   KernelArgs a = base;
-  a.defer_min_len = cfg.fused_stores == 1 ? kNoDefer : (cfg.fused_stores == 2 ? 0u : kDeferMinLen);
+  a.defer_min_len = cfg.fused_stores == 1 ? kNoDefer : (cfg.fused_stores >= 2 ? 0u : kDeferMinLen);
+  if (cfg.fused_stores == 3) a.no_scatter = 1;   // records only: the caller applies the checks
   return v->fn(a, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
 }
 

@@ -1,0 +1,260 @@
+// checksummer_app.c -- the checksummer NF on the MI355X batch path.
+//
+// Same command line and output as the reference app
+// (examples/checksummer/checksummer_user.c:113-260 with
+// examples/common/statistics.c): `checksummer [XSKNF_OPTIONS] -- [APP_OPTIONS]`,
+// -c REDIRECT|DROP, -i iterations, -q, -x, -a; per-second socket stats;
+// cumulative rx written to ./stats.txt on SIGUSR1.  The per-frame callback
+// (checksummer_user.c:30-112) is replaced by the GPU batch hook of
+// libxsknf_gpu: every rx batch is checksummed by one gfx950 launch.
+//
+// Extra app option: -g, --gpu-path=ZEROCOPY|STAGED (include/xsknf_gpu.h).
+// MODE_XDP / MODE_COMBINED need the NF's eBPF object and are not supported.
+#define _GNU_SOURCE
+
+#include <errno.h>
+#include <getopt.h>
+#include <libgen.h>
+#include <locale.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "../../include/xsknf.h"
+#include "../../include/xsknf_gpu.h"
+
+#define NSTATS 13   // counters in struct xsknf_socket_stats
+
+static int opt_action = XSKNF_CSUM_ACTION_REDIRECT;
+static int opt_csum_iterations = 1;
+static int opt_quiet, opt_extra_stats, opt_app_stats;
+static int opt_gpu_path = XSKNF_GPU_PATH_ZEROCOPY;
+static volatile sig_atomic_t benchmark_done, stats_requested;
+static struct xsknf_config config;
+
+static const struct option long_options[] = {
+	{"action", required_argument, 0, 'c'},
+	{"csum-iterations", required_argument, 0, 'i'},
+	{"quiet", no_argument, 0, 'q'},
+	{"extra-stats", no_argument, 0, 'x'},
+	{"app-stats", no_argument, 0, 'a'},
+	{"gpu-path", required_argument, 0, 'g'},
+	{0, 0, 0, 0},
+};
+
+static void usage(const char *prog)
+{
+	fprintf(stderr,
+		"  Usage: %s [XSKNF_OPTIONS] -- [APP_OPTIONS]\n"
+		"  App options:\n"
+		"  -c, --action		REDIRECT or DROP packets (default REDIRECT).\n"
+		"  -i, --csum-iterations	Number of times to recompute the checksum.\n"
+		"  -q, --quiet		Do not display any stats.\n"
+		"  -x, --extra-stats	Display extra statistics.\n"
+		"  -a, --app-stats	Display application (syscall) statistics.\n"
+		"  -g, --gpu-path	ZEROCOPY (default) or STAGED host path to the GPU.\n"
+		"\n",
+		prog);
+	exit(EXIT_FAILURE);
+}
+
+static void parse_command_line(int argc, char **argv, char *app_path)
+{
+	int option_index, c;
+	while ((c = getopt_long(argc, argv, "qxai:c:g:", long_options, &option_index)) != -1) {
+		switch (c) {
+		case 'c':
+			if (!strcmp(optarg, "REDIRECT")) {
+				opt_action = XSKNF_CSUM_ACTION_REDIRECT;
+			} else if (!strcmp(optarg, "DROP")) {
+				opt_action = XSKNF_CSUM_ACTION_DROP;
+			} else {
+				fprintf(stderr, "ERROR: invalid action %s\n", optarg);
+				usage(basename(app_path));
+			}
+			break;
+		case 'i':
+			opt_csum_iterations = atoi(optarg);
+			break;
+		case 'q':
+			opt_quiet = 1;
+			break;
+		case 'x':
+			opt_extra_stats = 1;
+			break;
+		case 'a':
+			opt_app_stats = 1;
+			break;
+		case 'g':
+			if (!strcmp(optarg, "ZEROCOPY")) {
+				opt_gpu_path = XSKNF_GPU_PATH_ZEROCOPY;
+			} else if (!strcmp(optarg, "STAGED")) {
+				opt_gpu_path = XSKNF_GPU_PATH_STAGED;
+			} else {
+				fprintf(stderr, "ERROR: invalid gpu path %s\n", optarg);
+				usage(basename(app_path));
+			}
+			break;
+		default:
+			usage(basename(app_path));
+		}
+	}
+}
+
+/* ---- statistics (examples/common/statistics.c:33-260) ---- */
+
+static struct xsknf_socket_stats old_stats[XSKNF_MAX_WORKERS][XSKNF_MAX_INTERFACES];
+static unsigned long prev_time;
+
+static unsigned long get_nsecs(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1000000000UL + ts.tv_nsec;
+}
+
+static void print_socket_stats(const unsigned long *cur, const double *ps, unsigned long dt)
+{
+	static const char *const names[NSTATS] = {
+		"rx", "tx", "rx dropped", "rx invalid", "tx invalid", "rx queue full",
+		"fill ring empty", "tx ring empty", "rx empty polls", "fill fail polls",
+		"tx wakeup sendtos", "tx trigger sendtos", "opt polls",
+	};
+	const char *fmt = "%-18s %'-14.0f %'-14lu\n";
+	printf("%-14s %-14s %-14.2f\n", "pps", "pkts", dt / 1000000000.);
+	for (int i = 0; i < 2; i++)
+		printf(fmt, names[i], ps[i], cur[i]);
+	if (opt_extra_stats)
+		for (int i = 2; i < 8; i++)
+			printf(fmt, names[i], ps[i], cur[i]);
+	if (opt_app_stats) {
+		printf("%-18s %-14s %-14s\n", "", "calls/s", "count");
+		for (int i = 8; i < NSTATS; i++)
+			printf(fmt, names[i], ps[i], cur[i]);
+	}
+}
+
+static void dump_stats(void)
+{
+	const unsigned long now = get_nsecs();
+	const unsigned long dt = now - prev_time;
+	unsigned long total[NSTATS] = {0};
+	double total_ps[NSTATS] = {0};
+	prev_time = now;
+	for (unsigned w = 0; w < config.workers; w++) {
+		for (unsigned j = 0; j < config.num_interfaces; j++) {
+			struct xsknf_socket_stats s;
+			if (xsknf_get_socket_stats(w, j, &s))
+				continue;
+			const unsigned long *cur = (const unsigned long *)&s;
+			const unsigned long *old = (const unsigned long *)&old_stats[w][j];
+			double ps[NSTATS];
+			for (int i = 0; i < NSTATS; i++) {
+				ps[i] = (cur[i] - old[i]) * 1000000000. / dt;
+				total[i] += cur[i];
+				total_ps[i] += ps[i];
+			}
+			char buf[256];
+			snprintf(buf, sizeof(buf), " %s@wrk%u", config.interfaces[j], w);
+			printf("\n%-19s", buf);
+			print_socket_stats(cur, ps, dt);
+			old_stats[w][j] = s;
+		}
+	}
+	printf("\n%-19s", " TOTAL");
+	print_socket_stats(total, total_ps, dt);
+	fflush(stdout);
+}
+
+// SIGUSR1: cumulative rx packets to ./stats.txt (statistics.c:219-264)
+static void write_stats_file(void)
+{
+	unsigned long total_rx = 0;
+	for (unsigned w = 0; w < config.workers; w++)
+		for (unsigned j = 0; j < config.num_interfaces; j++) {
+			struct xsknf_socket_stats s;
+			if (!xsknf_get_socket_stats(w, j, &s))
+				total_rx += s.rx_npkts;
+		}
+	FILE *f = fopen("./stats.txt", "w");
+	if (!f) {
+		perror("stats.txt");
+		return;
+	}
+	fprintf(f, "%lu\n", total_rx);
+	fclose(f);
+}
+
+static void int_exit(int sig)
+{
+	(void)sig;
+	benchmark_done = 1;
+}
+
+static void int_usr(int sig)
+{
+	(void)sig;
+	stats_requested = 1;
+}
+
+int main(int argc, char **argv)
+{
+	signal(SIGINT, int_exit);
+	signal(SIGTERM, int_exit);
+	signal(SIGABRT, int_exit);
+	signal(SIGUSR1, int_usr);
+
+	xsknf_parse_args(argc, argv, &config);
+	int rc = xsknf_init(&config, NULL);
+	if (rc) {
+		fprintf(stderr, "ERROR: xsknf_init: %s\n", strerror(-rc));
+		return EXIT_FAILURE;
+	}
+	parse_command_line(argc, argv, argv[0]);
+	setlocale(LC_ALL, "");
+
+	const struct xsknf_csum_opts opts = {
+		.csum_iterations = opt_csum_iterations,
+		.action = opt_action,
+		.num_interfaces = config.num_interfaces,
+	};
+	struct xsknf_gpu_hook *hook = NULL;
+	rc = xsknf_gpu_hook_create(&hook, &opts, config.workers, opt_gpu_path, config.batch_size,
+			(uint32_t)config.xsk_frame_size);
+	if (rc) {
+		fprintf(stderr, "ERROR: GPU hook: %s (%s)\n", strerror(-rc), xsknf_gpu_last_error());
+		xsknf_cleanup();
+		return EXIT_FAILURE;
+	}
+	xsknf_set_batch_processor((xsknf_batch_processor_fn)xsknf_gpu_hook_process, hook);
+	rc = xsknf_start_workers();
+	if (rc) {
+		fprintf(stderr, "ERROR: xsknf_start_workers: %s\n", strerror(-rc));
+		xsknf_gpu_hook_destroy(hook);
+		xsknf_cleanup();
+		return EXIT_FAILURE;
+	}
+	prev_time = get_nsecs();
+
+	int err = 0;
+	while (!benchmark_done && !err) {
+		sleep(1);
+		if (stats_requested) {
+			stats_requested = 0;
+			write_stats_file();
+		}
+		if (!opt_quiet)
+			dump_stats();
+		for (unsigned w = 0; w < config.workers && !err; w++)
+			err = xsknf_worker_error(w);
+	}
+	if (err)
+		fprintf(stderr, "ERROR: worker stopped: %s (%s)\n", strerror(-err), xsknf_gpu_last_error());
+	xsknf_stop_workers();
+	xsknf_gpu_hook_destroy(hook);
+	xsknf_cleanup();
+	return err ? EXIT_FAILURE : EXIT_SUCCESS;
+}

@@ -27,8 +27,8 @@ struct KernelArgs {
 // Check record parked in verdicts[f] by the summing pass (deferred stores):
 // tag 01 in bits 31..30 (no verdict, -1 or 0..XSKNF_MAX_INTERFACES-1, has it),
 // u in bits 22..16, the new check in bits 15..0.
-constexpr uint32_t kRecTag = 0x40000000u;
-constexpr uint32_t kRecTagMask = 0xC0000000u;
+constexpr uint32_t kRecTag = XSKNF_GPU_RECORD_TAG;
+constexpr uint32_t kRecTagMask = XSKNF_GPU_RECORD_TAG_MASK;
 constexpr uint32_t kNoDefer = 0xffffffffu;   // defer_min_len: every check in-line
 
 // Validate arguments and fill `a` (returns 1 for an empty batch, <0 on error).

@@ -159,8 +159,7 @@ int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *c, const struct xsknf_gpu_
       if (e != hipSuccess) return fail(e, "hipMemcpyAsync(umem span)");
       c->stats.bytes_h2d += hi - lo;
     }
-    cfg.fused_stores = 2;   // every check deferred ...
-    a.no_scatter = 1;       // ... and applied on the host below
+    cfg.fused_stores = 3;   // records only: the checks are applied on the host below
   } else {
     cfg.fused_stores = 1;   // in place over PCIe
   }
@@ -201,6 +200,124 @@ int xsknf_gpu_ctx_get_stats(const struct xsknf_gpu_ctx *c, struct xsknf_gpu_ctx_
 int xsknf_gpu_ctx_destroy(struct xsknf_gpu_ctx *c) {
   if (!c) return -EINVAL;
   release(c);
+  return 0;
+}
+
+}  // extern "C"
+
+// ---- batch hook: one context per (worker, UMEM) ------------------------------
+
+namespace {
+
+constexpr int kUmemsPerWorker = 2;  // a worker's zero-copy and copy-mode UMEMs
+
+struct HookSlot {
+  void *umem = nullptr;
+  xsknf_gpu_ctx *ctx = nullptr;
+};
+
+struct HookWorker {
+  HookSlot slot[kUmemsPerWorker];
+} __attribute__((aligned(64)));   // workers write their own slots only
+
+}  // namespace
+
+struct xsknf_gpu_hook {
+  xsknf_csum_opts opts = {};
+  uint32_t workers = 0;
+  int path = XSKNF_GPU_PATH_ZEROCOPY;
+  uint32_t max_batch = 0;
+  uint32_t hint = 0;
+  int devices = 1;
+  HookWorker *w = nullptr;
+};
+
+extern "C" {
+
+int xsknf_gpu_hook_create(struct xsknf_gpu_hook **out, const struct xsknf_csum_opts *opts, uint32_t workers,
+                          int path, uint32_t max_batch, uint32_t frame_len_hint) {
+  if (!out || !opts || workers == 0 || max_batch == 0) return -EINVAL;
+  if (path != XSKNF_GPU_PATH_ZEROCOPY && path != XSKNF_GPU_PATH_STAGED) return -EINVAL;
+  if (opts->action != XSKNF_CSUM_ACTION_REDIRECT && opts->action != XSKNF_CSUM_ACTION_DROP) return -EINVAL;
+  *out = nullptr;
+  int devices = 0;
+  hipError_t e = hipGetDeviceCount(&devices);
+  if (e != hipSuccess) return fail(e, "hipGetDeviceCount");
+  if (devices < 1) return -ENODEV;
+  xsknf_gpu_hook *h = new (std::nothrow) xsknf_gpu_hook;
+  if (!h) return -ENOMEM;
+  h->w = new (std::nothrow) HookWorker[workers];
+  if (!h->w) {
+    delete h;
+    return -ENOMEM;
+  }
+  h->opts = *opts;
+  h->workers = workers;
+  h->path = path;
+  h->max_batch = max_batch;
+  h->hint = frame_len_hint;
+  h->devices = devices;
+  *out = h;
+  return 0;
+}
+
+int xsknf_gpu_hook_process(void *hook, uint32_t worker_idx, void *umem, uint64_t umem_size,
+                           const struct xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
+                           int32_t *verdicts) {
+  xsknf_gpu_hook *h = static_cast<xsknf_gpu_hook *>(hook);
+  if (!h || worker_idx >= h->workers || !umem || umem_size == 0) return -EINVAL;
+  if (n > h->max_batch) return -EINVAL;
+  HookWorker &w = h->w[worker_idx];
+  xsknf_gpu_ctx *ctx = nullptr;
+  for (HookSlot &s : w.slot) {
+    if (s.umem == umem) {
+      ctx = s.ctx;
+      break;
+    }
+  }
+  if (!ctx) {
+    HookSlot *free_slot = nullptr;
+    for (HookSlot &s : w.slot) {
+      if (!s.umem) {
+        free_slot = &s;
+        break;
+      }
+    }
+    if (!free_slot) return -ENOSPC;
+    int rc = xsknf_gpu_ctx_create(&ctx, static_cast<int>(worker_idx % static_cast<uint32_t>(h->devices)),
+                                  h->path, h->max_batch, h->hint);
+    if (rc) return rc;
+    rc = xsknf_gpu_ctx_register_umem(ctx, umem, umem_size);
+    if (rc) {
+      xsknf_gpu_ctx_destroy(ctx);
+      return rc;
+    }
+    free_slot->umem = umem;
+    free_slot->ctx = ctx;
+  }
+  return xsknf_gpu_ctx_process_batch(ctx, descs, n, ingress_ifindex, &h->opts, verdicts);
+}
+
+int xsknf_gpu_hook_get_stats(const struct xsknf_gpu_hook *h, uint32_t worker_idx, struct xsknf_gpu_ctx_stats *stats) {
+  if (!h || !stats || worker_idx >= h->workers) return -EINVAL;
+  *stats = {};
+  for (const HookSlot &s : h->w[worker_idx].slot) {
+    if (!s.ctx) continue;
+    stats->batches += s.ctx->stats.batches;
+    stats->frames += s.ctx->stats.frames;
+    stats->bytes_h2d += s.ctx->stats.bytes_h2d;
+    stats->bytes_d2h += s.ctx->stats.bytes_d2h;
+  }
+  return 0;
+}
+
+int xsknf_gpu_hook_destroy(struct xsknf_gpu_hook *h) {
+  if (!h) return -EINVAL;
+  for (uint32_t i = 0; i < h->workers; ++i)
+    for (HookSlot &s : h->w[i].slot)
+      if (s.ctx) release(s.ctx);
+  delete[] h->w;
+  delete h;
   return 0;
 }
 
