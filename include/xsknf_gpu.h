@@ -107,7 +107,9 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * frame offset u + 6, verdict = the forward verdict"; frames that are not
  * summed carry their final verdict.  The STAGED host path uses this mode (the
  * host applies the checks); benchmarks use it to time the summing kernel.
- * Only instantiated shapes are accepted (-EINVAL
+ * In-line checks whose 64-byte sector lies inside the frame are written as
+ * that whole sector (register kernel); adding 4 to `fused_stores` writes the 2
+ * check bytes alone instead (A/B).  Only instantiated shapes are accepted (-EINVAL
  * otherwise); every shape gives identical results.
  */
 #define XSKNF_GPU_RECORD_TAG 0x40000000u       /* bits 31..30 = 01 */

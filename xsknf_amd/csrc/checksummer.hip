@@ -103,6 +103,25 @@ __device__ __forceinline__ uint4 load_nt(const uint4 *p) {
   return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+__device__ __forceinline__ void store_nt16(uint8_t *p, uint4 v) {
+  u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
+}
+
+// v with byte i (0..15) replaced by b; i outside 0..15 leaves v unchanged
+__device__ __forceinline__ uint4 put_byte(uint4 v, int i, uint32_t b) {
+  const uint32_t sh = 8u * (i & 3);
+  const uint32_t keep = ~(0xffu << sh), put = (b & 0xffu) << sh;
+  const int w = i >> 2;
+  if (i >= 0 && i < 16) {
+    v.x = w == 0 ? ((v.x & keep) | put) : v.x;
+    v.y = w == 1 ? ((v.y & keep) | put) : v.y;
+    v.z = w == 2 ? ((v.z & keep) | put) : v.z;
+    v.w = w == 3 ? ((v.w & keep) | put) : v.w;
+  }
+  return v;
+}
+
 // 0x01 in every byte b of the dword at window offset x with lo <= x+b < hi
 // (bytes [a, b) of a dword, a/b clamped to 0..4: two 64-bit shifts of 0x01010101).
 __device__ __forceinline__ uint32_t byte_ones(int lo, int hi, int x) {
@@ -159,6 +178,14 @@ __device__ __forceinline__ uint32_t group_sum_last(uint32_t v) {
   if constexpr (LPF >= 32) v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
   if constexpr (LPF >= 64) v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
   return v;
+}
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// The group's last lane's value on every lane of the group.
+template <int LPF>
+__device__ __forceinline__ uint32_t group_bcast_last(uint32_t v, int lane) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute((lane | (LPF - 1)) << 2, static_cast<int>(v)));
 }
 
 // ---- kernel arguments, frame references, descriptors -----------------------
@@ -259,13 +286,41 @@ __device__ __forceinline__ uint16_t check_of(const Header &h, uint32_t P, uint32
 // The word this frame leaves in verdicts[f] after the summing pass; the check
 // bytes are written here only in single-pass (fused) mode.
 __device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const FrameRef &r, const Header &h,
-                                                int32_t verdict, bool do_sum, uint32_t P) {
+                                                int32_t verdict, bool do_sum, uint32_t P,
+                                                bool sector_done = false) {
   if (!do_sum) return verdict;
   const uint16_t c = check_of(h, P, a.payload_mult);
   if (static_cast<uint32_t>(r.len) >= a.defer_min_len)
     return static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
-  *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+  if (!sector_done) *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
   return verdict;
+}
+
+// In-line check as a whole-sector rewrite (register kernel, pass-0 frames):
+// when the check's 64-byte sector lies inside the frame, the (up to 4) lanes
+// whose 16-byte chunks make up that sector patch the check bytes into the
+// chunk they loaded and store it back non-temporally -- one full-sector write
+// instead of a 2-byte partial write, which HBM turns into read-modify-write.
+// Returns true (on every lane of the group) when the sector was written.
+template <int LPF, int NCH>
+__device__ __forceinline__ bool store_check_sector(const FrameRef &r, const Header &h, uint16_t c,
+                                                   const uint4 (&v)[NCH], int gl) {
+  const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
+  const uintptr_t ck = f0 + h.u + 6;
+  const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
+  if (sec < f0 || sec + 64 > f0 + r.len || (ck & 63) == 63) return false;
+  const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const uintptr_t piece = c0 + 16u * static_cast<uint32_t>(k * LPF + gl);
+    if (piece >= sec && piece < sec + 64) {
+      const int o = static_cast<int>(static_cast<intptr_t>(ck - piece));
+      uint4 w = put_byte(v[k], o, c);
+      w = put_byte(w, o + 1, c >> 8);
+      store_nt16(r.fp + static_cast<intptr_t>(piece - f0), w);   // global addressing from fp
+    }
+  }
+  return true;
 }
 
 // Frames longer than one pass.  The pipelined step only sums pass 0 and parks
@@ -281,12 +336,12 @@ constexpr uint32_t kDeferMinLen = 1024;        // hybrid default (tools/tune.py:
 // Result word of a frame after its pass-0 sum P0 (group-reduced, last lane).
 __device__ __forceinline__ int32_t step_result(const KernelArgs &a, const FrameRef &r, const Header &h,
                                                int32_t verdict, bool do_sum, uint32_t P0, int span,
-                                               uint32_t part_addr) {
+                                               uint32_t part_addr, bool sector_done = false) {
   if (do_sum && r.nch > span) {
     lds_store_u32(part_addr, h.pseudo + a.payload_mult * (P0 - h.old_check));
     return static_cast<int32_t>(kPendTag | static_cast<uint32_t>(h.u));
   }
-  return frame_result(a, r, h, verdict, do_sum, P0);
+  return frame_result(a, r, h, verdict, do_sum, P0, sector_done);
 }
 
 // Finish the PENDING frames of a tile: passes 1.. of each, then their result.
@@ -372,7 +427,15 @@ __device__ __forceinline__ int32_t process_regs(const KernelArgs &args, const Fr
 #pragma unroll
   for (int k = 0; k < NCH; ++k) chunk_sum_fast(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
   const uint32_t P0 = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
-  return (gl == LPF - 1 && r.exists) ? step_result(args, r, h, verdict, do_sum, P0, LPF * NCH, part_addr) : 0;
+  bool sector_done = false;
+  if (args.sector_stores && __builtin_amdgcn_ballot_w64(do_sum && r.nch <= LPF * NCH &&
+                                                        static_cast<uint32_t>(r.len) < args.defer_min_len)) {
+    const uint32_t P = group_bcast_last<LPF>(P0, lane_id());
+    if (do_sum && r.nch <= LPF * NCH && static_cast<uint32_t>(r.len) < args.defer_min_len)
+      sector_done = store_check_sector<LPF, NCH>(r, h, check_of(h, P, args.payload_mult), v, gl);
+  }
+  return (gl == LPF - 1 && r.exists)
+             ? step_result(args, r, h, verdict, do_sum, P0, LPF * NCH, part_addr, sector_done) : 0;
 }
 
 template <int LPF, int NCH, int SPT>
@@ -572,48 +635,81 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
 // per frame.  Otherwise (sector crosses the frame edge, or the check straddles
 // two sectors) it writes the 2 check bytes alone.  Only this frame's own bytes
 // are ever rewritten (with their own values), so frames never race.
-
-__device__ __forceinline__ void store_nt16(uint8_t *p, uint4 v) {
-  u32x4 x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
-}
+//
+// Records are found by a scan with one lane per frame; each wave then ballots
+// its 64 frames and rewrites only the records, 16 per round (4 lanes each), so
+// the pass costs in proportion to the records (IMIX: 1 frame in 12), not to n.
 
 __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) {
-  const uint32_t nthreads = gridDim.x * kBlock;
-  for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < 4 * args.n; t += nthreads) {
-    const uint32_t f = t >> 2;
-    const int piece = t & 3;
-    const uint32_t r = static_cast<uint32_t>(args.verdicts[f]);
-    if ((r & kRecTagMask) != kRecTag) continue;
-    const xsknf_gpu_desc d = args.descs[f];
-    uint8_t *fp = args.umem + umem_offset(d.addr);
-    uint8_t *chk = fp + ((r >> 16) & 0x7f) + 6;
-    const uint16_t c = static_cast<uint16_t>(r);
-    uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);   // keeps global addressing
-    const bool whole = sec >= fp && sec + 64 <= fp + d.len && (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
-    if (whole) {
-      uint8_t *mine = sec + 16 * piece;
-      uint4 v = load_nt(reinterpret_cast<const uint4 *>(mine));
-      const int o = static_cast<int>(chk - mine);          // check offset in my 16-B piece
-      if (o >= 0 && o < 16) {                              // low byte here (high byte too unless o == 15)
-        uint8_t b[16];
-        memcpy(b, &v, 16);
-        b[o] = static_cast<uint8_t>(c);
-        if (o + 1 < 16) b[o + 1] = static_cast<uint8_t>(c >> 8);
-        memcpy(&v, b, 16);
-      }
-      if (o == -1) {                                       // high byte lands at my first byte
-        uint8_t b[16];
-        memcpy(b, &v, 16);
-        b[0] = static_cast<uint8_t>(c >> 8);
-        memcpy(&v, b, 16);
-      }
-      store_nt16(mine, v);
-    } else if (piece == 0) {
-      chk[0] = static_cast<uint8_t>(c);
-      chk[1] = static_cast<uint8_t>(c >> 8);
+  constexpr int kRounds = kWave / 16;                  // 16 records per round, 4 lanes each
+  __shared__ uint8_t which[kWavesPerBlock][kWave];     // record rank -> lane
+  const int lane = threadIdx.x & (kWave - 1);
+  const int piece = lane & 3;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t waves = gridDim.x * kWavesPerBlock;
+  for (uint32_t base = (blockIdx.x * kWavesPerBlock + wv) * kWave; base < args.n; base += waves * kWave) {
+    const uint32_t f = base + lane;
+    const uint32_t r = f < args.n ? static_cast<uint32_t>(args.verdicts[f]) : 0u;
+    // the lane's own descriptor, loaded beside its record (not after the scan):
+    // record lanes hand it over below, so no round waits for a descriptor load
+    const xsknf_gpu_desc own = args.descs[f < args.n ? f : args.n - 1];
+    const bool rec = (r & kRecTagMask) == kRecTag;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(rec);
+    if (!m) continue;
+    const int nrec = __builtin_popcountll(m);
+    if (rec) {
+      const int rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+      which[wv][rank] = static_cast<uint8_t>(lane);
     }
-    if (piece == 0) args.verdicts[f] = args.fwd_verdict;
+    __builtin_amdgcn_wave_barrier();
+    // every round's loads are issued before any store: up to 4 independent
+    // record -> descriptor -> sector chains per lane
+    uint32_t rr[kRounds];
+    uint32_t fi[kRounds];
+    bool ok[kRounds];
+    xsknf_gpu_desc d[kRounds];
+    const uint32_t alo = static_cast<uint32_t>(own.addr), ahi = static_cast<uint32_t>(own.addr >> 32);
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      const int k = 16 * j + (lane >> 2);
+      const int src = which[wv][min(k, nrec - 1)] << 2;
+      rr[j] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(r)));
+      const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(alo)));
+      const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(ahi)));
+      d[j].addr = (static_cast<uint64_t>(hi) << 32) | lo;
+      d[j].len = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(own.len)));
+      fi[j] = base + (src >> 2);
+      ok[j] = k < nrec;
+    }
+    __builtin_amdgcn_wave_barrier();   // `which` is rewritten by the next chunk
+    uint8_t *mine[kRounds];
+    uint8_t *chk[kRounds];
+    bool whole[kRounds];
+    uint4 v[kRounds];
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      uint8_t *fp = args.umem + umem_offset(d[j].addr);
+      chk[j] = fp + ((rr[j] >> 16) & 0x7f) + 6;
+      uint8_t *sec = chk[j] - (reinterpret_cast<uintptr_t>(chk[j]) & 63);   // keeps global addressing
+      whole[j] = ok[j] && sec >= fp && sec + 64 <= fp + d[j].len && (reinterpret_cast<uintptr_t>(chk[j]) & 63) != 63;
+      mine[j] = sec + 16 * piece;
+      if (whole[j]) v[j] = load_nt(reinterpret_cast<const uint4 *>(mine[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      const uint16_t c = static_cast<uint16_t>(rr[j]);
+      if (whole[j]) {
+        const int o = static_cast<int>(chk[j] - mine[j]);   // check offset in my 16-B piece
+        uint4 w = put_byte(v[j], o, c);
+        w = put_byte(w, o + 1, c >> 8);
+        store_nt16(mine[j], w);
+      } else if (ok[j] && piece == 0) {
+        chk[j][0] = static_cast<uint8_t>(c);
+        chk[j][1] = static_cast<uint8_t>(c >> 8);
+      }
+      if (ok[j] && piece == 0) args.verdicts[fi[j]] = args.fwd_verdict;
+    }
   }
 }
 
@@ -671,7 +767,7 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
 int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && a.defer_min_len != kNoDefer && !a.no_scatter) {
-    const uint32_t need = (4 * a.n + kBlock - 1) / kBlock;
+    const uint32_t need = (a.n + kBlock - 1) / kBlock;   // one lane per frame
     const uint32_t cap = static_cast<uint32_t>(device_cus() * 8);
     hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
     e = hipGetLastError();
@@ -723,17 +819,24 @@ const Variant *find_variant(int lpf, int nch, int u, int ring) {
 
 // Default shape for a length hint.
 void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
-  c.frames_per_group = 1;
+  c.frames_per_group = 4;
   c.blocks_per_cu = 8;
-  c.fused_stores = 0;
   c.lds_ring = 0;
   // measured best per size class on MI355X (tools/tune.py, 1M-frame batches):
-  // up to ~1 KiB, 8 lanes per frame (longer frames finish their extra passes at
-  // tile end); 1500 B, 16 lanes x 2 chunks; jumbo frames, one wave per frame
-  if (hint <= 1024) { c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.frames_per_group = 4; }
-  else if (hint + 15 <= 2048) { c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.frames_per_group = 4; }
-  else if (hint + 15 <= 4096) { c.lanes_per_frame = 64; c.chunks_per_lane = 4; c.frames_per_group = 4; }
-  else { c.lanes_per_frame = 64; c.chunks_per_lane = 9; c.frames_per_group = 4; }
+  // up to ~1 KiB, 8 lanes per frame, every check in-line as a whole-sector
+  // rewrite and no scatter pass (64 B: 60 us vs 77 us with 2-byte stores + the
+  // pass); 1500 B, 16 lanes x 2 chunks with long frames' checks deferred and the
+  // short ones of a mix written as 2 bytes (whole sectors cost IMIX ~10 %);
+  // jumbo frames, one wave per frame
+  if (hint <= 1024) {
+    c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.fused_stores = 1;
+  } else if (hint + 15 <= 2048) {
+    c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.fused_stores = 4;
+  } else if (hint + 15 <= 4096) {
+    c.lanes_per_frame = 64; c.chunks_per_lane = 4; c.fused_stores = 4;
+  } else {
+    c.lanes_per_frame = 64; c.chunks_per_lane = 9; c.fused_stores = 4;
+  }
 }
 
 int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_desc *descs, uint32_t n,
@@ -754,6 +857,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
                       : -1;
   a.defer_min_len = kDeferMinLen;
   a.no_scatter = 0;
+  a.sector_stores = 1;
   // aligned-down descriptor address: inside the descriptor array's own page
   a.dummy = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(descs) & ~static_cast<uintptr_t>(15));
   return 0;
@@ -761,12 +865,14 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
 
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
-  if (cfg.fused_stores < 0 || cfg.fused_stores > 3) return -EINVAL;
+  const int mode = cfg.fused_stores & 3;          // + 4: 2-byte in-line stores
+  if (cfg.fused_stores < 0 || cfg.fused_stores > 7) return -EINVAL;
   const Variant *v = find_variant(cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group, cfg.lds_ring);
   if (!v) return -EINVAL;
   KernelArgs a = base;
-  a.defer_min_len = cfg.fused_stores == 1 ? kNoDefer : (cfg.fused_stores >= 2 ? 0u : kDeferMinLen);
-  if (cfg.fused_stores == 3) a.no_scatter = 1;   // records only: the caller applies the checks
+  a.defer_min_len = mode == 1 ? kNoDefer : (mode >= 2 ? 0u : kDeferMinLen);
+  if (mode == 3) a.no_scatter = 1;   // records only: the caller applies the checks
+  if (cfg.fused_stores & 4) a.sector_stores = 0;
   return v->fn(a, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
 }
 

@@ -22,6 +22,9 @@ struct KernelArgs {
   const uint4 *dummy;      // readable 16-byte block for frames that need no bytes
   uint32_t no_scatter;     // 1: leave deferred check records in `verdicts` (the host
                            // path applies them itself)
+  uint32_t sector_stores;  // 1: an in-line check whose 64-byte sector lies inside the
+                           // frame is written as that whole sector (device memory:
+                           // no read-modify-write); 0: 2-byte stores (host memory)
 };
 
 // Check record parked in verdicts[f] by the summing pass (deferred stores):

@@ -161,7 +161,8 @@ int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *c, const struct xsknf_gpu_
     }
     cfg.fused_stores = 3;   // records only: the checks are applied on the host below
   } else {
-    cfg.fused_stores = 1;   // in place over PCIe
+    cfg.fused_stores = 1;   // in place over PCIe, ...
+    a.sector_stores = 0;    // ... as 2-byte writes (byte enables; no RMW in host memory)
   }
   rc = run(a, cfg, c->stream);
   if (rc != 0) return rc;
