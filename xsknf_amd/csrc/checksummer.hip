@@ -35,6 +35,7 @@
 //   tools/hbm_probe), it parks check records in `verdicts`; a write-only
 //   scatter pass then writes the 2 check bytes per frame and the verdicts.
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <errno.h>
 #include <stdio.h>
@@ -383,12 +384,54 @@ __device__ __forceinline__ void finish_long_frames(const KernelArgs &a, uint32_t
   }
 }
 
+// Records per launch, for the scatter pass to pick its shape (per device: a
+// __device__ variable exists once per GPU).  Launch `seq` adds to set seq % 8
+// and clears set (seq + 4) % 8 for a later launch.  A set is 64 counters on
+// separate 64-byte lines (block b adds to counter b % 64): one shared address
+// would serialize every tile's atomic in one L2 channel.  Only speed depends on
+// the count: both scatter shapes are exact at any record density.
+constexpr uint32_t kCountSlots = 8;
+constexpr uint32_t kCountLanes = 64;
+constexpr uint32_t kCountStride = 16;          // u32 words = 64 bytes
+__device__ uint32_t g_rec_count[kCountSlots][kCountLanes][kCountStride];
+
+// Store a tile's result word (lane's frame); returns the tile's record count
+// (wave-uniform), which the wave adds up and publishes once, at exit: an
+// atomic per tile would hold every following vmcnt wait on its L2 round trip.
+__device__ __forceinline__ uint32_t store_result(const KernelArgs &a, uint32_t f, bool valid, int32_t v) {
+  if (valid) a.verdicts[f] = v;
+  if (!a.count_records) return 0;
+  return static_cast<uint32_t>(__builtin_popcountll(
+      __builtin_amdgcn_ballot_w64(valid && (static_cast<uint32_t>(v) & kRecTagMask) == kRecTag)));
+}
+
+__device__ __forceinline__ void publish_records(const KernelArgs &a, uint32_t nrec, int lane) {
+  if (a.count_records && lane == 0 && nrec)
+    atomicAdd(&g_rec_count[a.seq % kCountSlots][blockIdx.x % kCountLanes][0], nrec);
+}
+
+__device__ __forceinline__ void clear_next_count(const KernelArgs &a) {
+  if (a.count_records && blockIdx.x == 0 && threadIdx.x < kCountLanes)
+    g_rec_count[(a.seq + 4) % kCountSlots][threadIdx.x][0] = 0;
+}
+
+// The launch's record count, on every lane (wave-wide sum of the 64 counters).
+__device__ __forceinline__ uint32_t launch_records(const KernelArgs &a) {
+  const int lane = threadIdx.x & (kWave - 1);
+  uint32_t c = __hip_atomic_load(&g_rec_count[a.seq % kCountSlots][lane % kCountLanes][0], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c += static_cast<uint32_t>(__shfl_xor(static_cast<int>(c), o, kWave));
+  return c;
+}
+
 // Write a finished tile's results (LDS rec[0..63]) as one coalesced store.
-__device__ __forceinline__ void flush_tile(const KernelArgs &a, uint32_t rec, uint32_t tile_f0, int lane) {
+__device__ __forceinline__ uint32_t flush_tile(const KernelArgs &a, uint32_t rec, uint32_t tile_f0, int lane) {
   compiler_barrier();
   const int32_t v = lds_i32(rec + 4 * lane);
-  if (tile_f0 + lane < a.n) a.verdicts[tile_f0 + lane] = v;
+  const uint32_t nrec = store_result(a, tile_f0 + lane, tile_f0 + lane < a.n, v);
   compiler_barrier();
+  return nrec;
 }
 
 // ---- register kernel ----------------------------------------------------------
@@ -461,9 +504,11 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
   const uint32_t dsc = lds_addr(&dtile[wv][0]);
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t last = args.n - 1;
+  clear_next_count(args);
 
   // the next tile's descriptors ride in VGPRs (lane l: frame l of the tile)
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
+  uint32_t nrec = 0;                         // records this wave parked (wave-uniform)
   uint4 dnext = *reinterpret_cast<const uint4 *>(args.descs + min(tile * T + min(lane, T - 1), last));
   for (; tile * T < args.n; tile += waves) {
     const uint32_t tf0 = tile * T;
@@ -494,9 +539,10 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
     compiler_barrier();
     finish_long_frames<LPF, NCH>(args, dsc, tf0, rec, part, SPT, grp, gl);
     compiler_barrier();
-    if (lane < T && tf0 + lane < args.n) args.verdicts[tf0 + lane] = lds_i32(rec + 4 * lane);
+    nrec += store_result(args, tf0 + lane, lane < T && tf0 + lane < args.n, lds_i32(rec + 4 * min(lane, T - 1)));
     compiler_barrier();
   }
+  publish_records(args, nrec, lane);
 }
 
 // ---- LDS-DMA ring kernel ------------------------------------------------------
@@ -552,6 +598,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t wg = blockIdx.x * kWavesPerBlock + wv;
   const uint32_t last = args.n - 1;
+  clear_next_count(args);
 
   // Step j of this wave covers tile k = j / SPT (global tile wg + k*waves),
   // frames (j % SPT)*G + grp of it.  Tile k's descriptors sit in dtile[k & 1],
@@ -580,12 +627,14 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
   }
 
   uint32_t j = 0;
+  uint32_t nrec = 0;                    // records this wave parked (wave-uniform)
   while (true) {
 #pragma unroll
     for (int s = 0; s < R; ++s) {       // unrolled so ring slots and refs are static
       const uint32_t tk = j / SPT, js = j % SPT;
       const uint32_t f0 = tile_f0(tk);
       if (f0 >= args.n) {               // wave-uniform exit (tiles ascend)
+        publish_records(args, nrec, lane);
         wait_vmcnt<0>();                // no DMA may land after the workgroup ends
         return;
       }
@@ -616,7 +665,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
       if (js == SPT - 1) {             // steps past n ran as no-ops
         compiler_barrier();
         finish_long_frames<LPF, NCH>(args, dsc0 + (tk & 1) * (kTile * 16), f0, rec, part, SPT, grp, gl);
-        flush_tile(args, rec, f0, lane);
+        nrec += flush_tile(args, rec, f0, lane);
       }
       ++j;
     }
@@ -636,23 +685,54 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
 // two sectors) it writes the 2 check bytes alone.  Only this frame's own bytes
 // are ever rewritten (with their own values), so frames never race.
 //
-// Records are found by a scan with one lane per frame; each wave then ballots
-// its 64 frames and rewrites only the records, 16 per round (4 lanes each), so
-// the pass costs in proportion to the records (IMIX: 1 frame in 12), not to n.
+// Two shapes, picked per launch from the record count the summing kernel
+// leaves in g_rec_count: dense (4 lanes per frame over the grid) and sparse
+// (per-wave scan + compaction).
 
-__global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) {
-  constexpr int kRounds = kWave / 16;                  // 16 records per round, 4 lanes each
-  __shared__ uint8_t which[kWavesPerBlock][kWave];     // record rank -> lane
+// Rewrite one parked check: lane `piece` (0..3) of the record's 4 lanes.
+__device__ __forceinline__ void rewrite_check(const KernelArgs &args, uint32_t f, uint32_t r,
+                                              const xsknf_gpu_desc &d, int piece) {
+  uint8_t *fp = args.umem + umem_offset(d.addr);
+  uint8_t *chk = fp + ((r >> 16) & 0x7f) + 6;
+  const uint16_t c = static_cast<uint16_t>(r);
+  uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);   // keeps global addressing
+  const bool whole = sec >= fp && sec + 64 <= fp + d.len && (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
+  if (whole) {
+    uint8_t *mine = sec + 16 * piece;
+    const int o = static_cast<int>(chk - mine);          // check offset in my 16-B piece (-1..63)
+    uint4 v = load_nt(reinterpret_cast<const uint4 *>(mine));
+    v = put_byte(v, o, c);
+    v = put_byte(v, o + 1, c >> 8);
+    store_nt16(mine, v);
+  } else if (piece == 0) {
+    chk[0] = static_cast<uint8_t>(c);
+    chk[1] = static_cast<uint8_t>(c >> 8);
+  }
+  if (piece == 0) args.verdicts[f] = args.fwd_verdict;
+}
+
+// Dense records (>= 1/4 of the frames): 4 lanes per frame over the whole grid;
+// each lane's record and descriptor loads are independent of any scan.
+__device__ __forceinline__ void scatter_dense(const KernelArgs &args) {
+  const uint32_t nthreads = gridDim.x * kBlock;
+  for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < 4 * args.n; t += nthreads) {
+    const uint32_t f = t >> 2;
+    const uint32_t r = static_cast<uint32_t>(args.verdicts[f]);
+    const xsknf_gpu_desc d = args.descs[f];
+    if ((r & kRecTagMask) == kRecTag) rewrite_check(args, f, r, d, t & 3);
+  }
+}
+
+// Sparse records: one lane per frame scans; each wave ballots its 64 frames and
+// rewrites only its records, 16 per round (4 lanes each), so the pass costs in
+// proportion to the records (IMIX: 1 frame in 12), not to n.
+__device__ __forceinline__ void scatter_sparse(const KernelArgs &args, uint8_t *which) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int piece = lane & 3;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   for (uint32_t base = (blockIdx.x * kWavesPerBlock + wv) * kWave; base < args.n; base += waves * kWave) {
     const uint32_t f = base + lane;
     const uint32_t r = f < args.n ? static_cast<uint32_t>(args.verdicts[f]) : 0u;
-    // the lane's own descriptor, loaded beside its record (not after the scan):
-    // record lanes hand it over below, so no round waits for a descriptor load
-    const xsknf_gpu_desc own = args.descs[f < args.n ? f : args.n - 1];
     const bool rec = (r & kRecTagMask) == kRecTag;
     const uint64_t m = __builtin_amdgcn_ballot_w64(rec);
     if (!m) continue;
@@ -660,57 +740,26 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
     if (rec) {
       const int rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-      which[wv][rank] = static_cast<uint8_t>(lane);
+      which[rank] = static_cast<uint8_t>(lane);
     }
     __builtin_amdgcn_wave_barrier();
-    // every round's loads are issued before any store: up to 4 independent
-    // record -> descriptor -> sector chains per lane
-    uint32_t rr[kRounds];
-    uint32_t fi[kRounds];
-    bool ok[kRounds];
-    xsknf_gpu_desc d[kRounds];
-    const uint32_t alo = static_cast<uint32_t>(own.addr), ahi = static_cast<uint32_t>(own.addr >> 32);
-#pragma unroll
-    for (int j = 0; j < kRounds; ++j) {
-      const int k = 16 * j + (lane >> 2);
-      const int src = which[wv][min(k, nrec - 1)] << 2;
-      rr[j] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(r)));
-      const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(alo)));
-      const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(ahi)));
-      d[j].addr = (static_cast<uint64_t>(hi) << 32) | lo;
-      d[j].len = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(own.len)));
-      fi[j] = base + (src >> 2);
-      ok[j] = k < nrec;
+    for (int k0 = 0; k0 < nrec; k0 += kWave / 4) {
+      const int k = k0 + (lane >> 2);
+      const int src = which[min(k, nrec - 1)];
+      const uint32_t rs = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(r)));
+      if (k < nrec) rewrite_check(args, base + src, rs, args.descs[base + src], lane & 3);
     }
     __builtin_amdgcn_wave_barrier();   // `which` is rewritten by the next chunk
-    uint8_t *mine[kRounds];
-    uint8_t *chk[kRounds];
-    bool whole[kRounds];
-    uint4 v[kRounds];
-#pragma unroll
-    for (int j = 0; j < kRounds; ++j) {
-      uint8_t *fp = args.umem + umem_offset(d[j].addr);
-      chk[j] = fp + ((rr[j] >> 16) & 0x7f) + 6;
-      uint8_t *sec = chk[j] - (reinterpret_cast<uintptr_t>(chk[j]) & 63);   // keeps global addressing
-      whole[j] = ok[j] && sec >= fp && sec + 64 <= fp + d[j].len && (reinterpret_cast<uintptr_t>(chk[j]) & 63) != 63;
-      mine[j] = sec + 16 * piece;
-      if (whole[j]) v[j] = load_nt(reinterpret_cast<const uint4 *>(mine[j]));
-    }
-#pragma unroll
-    for (int j = 0; j < kRounds; ++j) {
-      const uint16_t c = static_cast<uint16_t>(rr[j]);
-      if (whole[j]) {
-        const int o = static_cast<int>(chk[j] - mine[j]);   // check offset in my 16-B piece
-        uint4 w = put_byte(v[j], o, c);
-        w = put_byte(w, o + 1, c >> 8);
-        store_nt16(mine[j], w);
-      } else if (ok[j] && piece == 0) {
-        chk[j][0] = static_cast<uint8_t>(c);
-        chk[j][1] = static_cast<uint8_t>(c >> 8);
-      }
-      if (ok[j] && piece == 0) args.verdicts[fi[j]] = args.fwd_verdict;
-    }
   }
+}
+
+__global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) {
+  __shared__ uint8_t which[kWavesPerBlock][kWave];     // record rank -> lane (sparse shape)
+  const uint32_t cnt = __builtin_amdgcn_readfirstlane(launch_records(args));
+  if (4ull * cnt >= args.n)
+    scatter_dense(args);
+  else
+    scatter_sparse(args, which[threadIdx.x / kWave]);
 }
 
 // ---- host side ----------------------------------------------------------------
@@ -767,7 +816,7 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
 int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && a.defer_min_len != kNoDefer && !a.no_scatter) {
-    const uint32_t need = (a.n + kBlock - 1) / kBlock;   // one lane per frame
+    const uint32_t need = (4 * a.n + kBlock - 1) / kBlock;   // dense shape: 4 lanes per frame
     const uint32_t cap = static_cast<uint32_t>(device_cus() * 8);
     hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
     e = hipGetLastError();
@@ -858,6 +907,8 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
   a.defer_min_len = kDeferMinLen;
   a.no_scatter = 0;
   a.sector_stores = 1;
+  a.seq = 0;
+  a.count_records = 0;
   // aligned-down descriptor address: inside the descriptor array's own page
   a.dummy = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(descs) & ~static_cast<uintptr_t>(15));
   return 0;
@@ -873,6 +924,9 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   a.defer_min_len = mode == 1 ? kNoDefer : (mode >= 2 ? 0u : kDeferMinLen);
   if (mode == 3) a.no_scatter = 1;   // records only: the caller applies the checks
   if (cfg.fused_stores & 4) a.sector_stores = 0;
+  static std::atomic<uint32_t> seq{0};
+  a.seq = seq.fetch_add(1, std::memory_order_relaxed);
+  a.count_records = a.defer_min_len != kNoDefer && !a.no_scatter;
   return v->fn(a, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
 }
 

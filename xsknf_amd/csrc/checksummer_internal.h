@@ -22,6 +22,8 @@ struct KernelArgs {
   const uint4 *dummy;      // readable 16-byte block for frames that need no bytes
   uint32_t no_scatter;     // 1: leave deferred check records in `verdicts` (the host
                            // path applies them itself)
+  uint32_t seq;            // launch sequence number: slot of the record counter
+  uint32_t count_records;  // 1: the summing kernel counts its records for the scatter pass
   uint32_t sector_stores;  // 1: an in-line check whose 64-byte sector lies inside the
                            // frame is written as that whole sector (device memory:
                            // no read-modify-write); 0: 2-byte stores (host memory)
