@@ -515,6 +515,16 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
     compiler_barrier();
     if (lane < T) lds_store_u128(dsc + 16 * lane, dnext);
     compiler_barrier();
+    // per-tile store policy: long frames defer their checks only where they are
+    // at least half of the tile (a 1500 B batch); in a mix (IMIX: 1 in 12) they
+    // write in-line, which is cheaper than a scatter pass for a few frames
+    KernelArgs ta = args;
+    if (args.defer_min_len != kNoDefer && args.defer_min_len != 0 && !args.no_scatter) {
+      const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
+          __builtin_amdgcn_ballot_w64(lane < T && tf0 + lane < args.n && dnext.z >= args.defer_min_len)));
+      const uint32_t nlive = min(static_cast<uint32_t>(T), args.n - tf0);
+      if (2 * nlong < nlive) ta.defer_min_len = kNoDefer;
+    }
     dnext = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * T + min(lane, T - 1), last));
 
     uint4 va[NCH], vb[NCH];
@@ -532,12 +542,12 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
         rn = ref_from_lds(args, dsc + 16 * i, tf0 + i);
         load_frame<LPF, NCH>(rn, gl, vn);
       }
-      const int32_t res = process_regs<LPF, NCH>(args, rc, vc, slot, gl, part + 4 * (st * G + grp));
+      const int32_t res = process_regs<LPF, NCH>(ta, rc, vc, slot, gl, part + 4 * (st * G + grp));
       if (gl == LPF - 1 && rc.exists) lds_store_i32(rec + 4 * (st * G + grp), res);
       compiler_barrier();   // the next frame rewrites this group's header window
     }
     compiler_barrier();
-    finish_long_frames<LPF, NCH>(args, dsc, tf0, rec, part, SPT, grp, gl);
+    finish_long_frames<LPF, NCH>(ta, dsc, tf0, rec, part, SPT, grp, gl);
     compiler_barrier();
     nrec += store_result(args, tf0 + lane, lane < T && tf0 + lane < args.n, lds_i32(rec + 4 * min(lane, T - 1)));
     compiler_barrier();
@@ -756,6 +766,7 @@ __device__ __forceinline__ void scatter_sparse(const KernelArgs &args, uint8_t *
 __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) {
   __shared__ uint8_t which[kWavesPerBlock][kWave];     // record rank -> lane (sparse shape)
   const uint32_t cnt = __builtin_amdgcn_readfirstlane(launch_records(args));
+  if (cnt == 0) return;                              // nothing parked (e.g. a mix written in-line)
   if (4ull * cnt >= args.n)
     scatter_dense(args);
   else
