@@ -87,7 +87,7 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
 
 /*
  * Launch shape of the batch kernel (tuning / benchmarking).  A group of
- * `lanes_per_frame` lanes (8, 16, 32 or 64) owns one frame at a time and loads
+ * `lanes_per_frame` lanes (4, 8, 16, 32 or 64) owns one frame at a time and loads
  * `chunks_per_lane` 16-byte chunks per pass; in the register kernel a wave
  * takes tiles of `frames_per_group` consecutive frames per group (the next
  * frame's loads in flight while the current one is reduced); the persistent
@@ -95,6 +95,10 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * 256-thread blocks per CU (0 = 8).  `lds_ring` > 0 selects the LDS-DMA
  * kernel, which streams each wave's frames through a ring of that many LDS
  * slots (frames_per_group is then ignored); 0 selects the register kernel.
+ * `lanes_per_frame` = 1 selects the lane kernel for small frames: each lane
+ * owns a frame, loads its first `chunks_per_lane` (5..7) chunks itself, and a
+ * wave step covers 64 frames (`frames_per_group` = steps per tile); longer
+ * frames are finished by a per-lane loop.
  * `fused_stores` = 1 writes every check from the summing kernel itself; 2 parks
  * every check for a second, write-only pass (non-temporal full 64-byte sector
  * rewrites); 0 (default) decides per frame: frames of 1024 bytes or more are
@@ -108,8 +112,9 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * summed carry their final verdict.  The STAGED host path uses this mode (the
  * host applies the checks); benchmarks use it to time the summing kernel.
  * In-line checks whose 64-byte sector lies inside the frame are written as
- * that whole sector (register kernel); adding 4 to `fused_stores` writes the 2
- * check bytes alone instead (A/B).  Only instantiated shapes are accepted (-EINVAL
+ * that whole sector (group and lane kernels); adding 4 to `fused_stores` writes
+ * the 2 check bytes alone instead, adding 8 makes the lane kernel's sector
+ * stores plain (write-back) rather than non-temporal (A/B).  Only instantiated shapes are accepted (-EINVAL
  * otherwise); every shape gives identical results.
  */
 #define XSKNF_GPU_RECORD_TAG 0x40000000u       /* bits 31..30 = 01 */

@@ -175,6 +175,9 @@ SHAPES = [
     (8, 1, 2, 0, 0), (8, 1, 8, 0, 1), (16, 2, 4, 0, 2), (32, 3, 4, 0, 1), (32, 3, 2, 0, 0),
     (64, 9, 2, 0, 2), (64, 2, 8, 0, 0), (8, 1, 1, 3, 2), (16, 2, 1, 3, 1), (32, 3, 1, 2, 0), (32, 3, 1, 3, 1),
     (64, 4, 1, 3, 0), (64, 2, 1, 4, 1),
+    (4, 2, 4, 0, 1), (4, 2, 2, 0, 0), (4, 2, 4, 0, 5),
+    # lane per frame (window 5..7 chunks; longer frames take the per-lane tail loop)
+    (1, 5, 2, 0, 1), (1, 5, 4, 0, 0), (1, 6, 2, 0, 9), (1, 7, 2, 0, 5), (1, 5, 2, 0, 2),
     # 2-byte in-line stores instead of whole-sector rewrites
     (8, 1, 4, 0, 5), (16, 2, 4, 0, 4), (32, 3, 4, 0, 5),
 ]

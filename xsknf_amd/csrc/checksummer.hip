@@ -86,6 +86,10 @@ __device__ __forceinline__ void lds_store_u128(uint32_t a, uint4 v) {
   *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(static_cast<uintptr_t>(a)) = x;
 }
 
+__device__ __forceinline__ void lds_store_u8(uint32_t a, uint8_t v) {
+  *reinterpret_cast<lds_u8 *>(static_cast<uintptr_t>(a)) = v;
+}
+
 __device__ __forceinline__ void lds_store_i32(uint32_t a, int32_t v) {
   *reinterpret_cast<__attribute__((address_space(3))) int32_t *>(static_cast<uintptr_t>(a)) = v;
 }
@@ -555,6 +559,165 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
   publish_records(args, nrec, lane);
 }
 
+// ---- lane-per-frame kernel (small frames) ---------------------------------------
+//
+// One lane owns a whole frame: it loads the frame's first NCH 16-byte chunks
+// itself, parses the header from its own LDS slot, sums with no cross-lane
+// reduction and writes its check from its own registers.  For 64 B frames the
+// group kernels spend most of their time on per-frame overhead (descriptor,
+// header, reduction for 8 frames per wave step); here a wave step covers 64
+// frames.  A wave works through tiles of SPT steps (64 * SPT consecutive frames)
+// with the two-buffer unrolled pipeline of the register kernel; the tile's
+// descriptors ride in registers, loaded one tile ahead.  Chunks past NCH (frames
+// longer than the window) are loaded and summed in a per-lane tail loop.
+
+constexpr int kLaneSlot = 16 * kHdrChunks;   // per-lane LDS header window
+
+// Default-policy loads: a lane's chunks of one frame arrive in NCH separate
+// (uncoalesced) instructions, and the line must stay in L2 between them (and
+// for the sector store that follows); non-temporal loads refetch it.
+template <int NCH>
+__device__ __forceinline__ void load_lane(const FrameRef &r, uint4 (&v)[NCH]) {
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) v[k] = r.cp[min(k, r.nch - 1)];
+}
+
+// A lane's result; when `sector` is set, the frame's patched 64-byte check
+// sector sits in the lane's LDS slot at `lds_sec`, to be written to `gsec` by
+// the wave's cooperative store (store_sectors).
+struct LaneOut {
+  int32_t res;
+  bool sector;
+  uint32_t lds_sec;
+  uint8_t *gsec;
+};
+
+template <int NCH>
+__device__ __forceinline__ LaneOut process_lane(const KernelArgs &args, const FrameRef &r, const uint4 (&v)[NCH],
+                                                uint32_t slot) {
+  static_assert(NCH >= 4 && NCH <= kHdrChunks, "lane window");
+  LaneOut out = {0, false, slot, r.fp};
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) lds_store_u128(slot + 16 * k, v[k]);
+  const int need = min(kHdrChunks, r.nch);   // header bytes past the window (large ihl)
+  for (int k = NCH; k < need; ++k) lds_store_u128(slot + 16 * k, r.cp[k]);
+  compiler_barrier();
+  const Header h = parse_header(slot + r.rs);
+  compiler_barrier();
+  bool do_sum;
+  const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
+  if (!r.exists) return out;
+  out.res = verdict;
+  if (!do_sum) return out;
+  const int lo = r.rs + h.u, hi = r.rs + r.len;
+  const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+  const uint32_t wh = wl << 8 | wl >> 24;
+  uint32_t acc_lo = 0, acc_hi = 0;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) chunk_sum(v[k], 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
+  for (int k = NCH; k < r.nch; ++k) chunk_sum(r.cp[k], 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
+  const uint16_t c = check_of(h, acc_lo + (acc_hi << 8), args.payload_mult);
+  if (static_cast<uint32_t>(r.len) >= args.defer_min_len) {
+    out.res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
+    return out;
+  }
+  // in-line: the whole 64-byte sector when it lies inside the frame and the
+  // window (patched in the LDS copy, stored by the wave), else the 2 bytes
+  const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
+  const uintptr_t ck = f0 + h.u + 6;
+  const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
+  const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
+  if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
+      sec + 64 <= c0 + 16 * NCH) {
+    const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
+    lds_store_u8(at, static_cast<uint8_t>(c));
+    lds_store_u8(at + 1, static_cast<uint8_t>(c >> 8));
+    out.sector = true;
+    out.lds_sec = slot + static_cast<uint32_t>(sec - c0);
+    out.gsec = r.fp + static_cast<intptr_t>(sec - f0);   // global addressing from fp
+  } else {
+    *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+  }
+  return out;
+}
+
+// The wave's patched sectors, 16 per instruction: lanes 4i..4i+3 write the 4
+// pieces of lane (16p + i)'s sector -- one coalesced 64-byte request each,
+// instead of 4 separate 16-byte stores per lane.
+__device__ __forceinline__ void store_sectors(const LaneOut &o, int lane, bool plain) {
+  const uint64_t any = __builtin_amdgcn_ballot_w64(o.sector);
+  if (!any) return;
+  compiler_barrier();
+  const uint32_t glo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o.gsec));
+  const uint32_t ghi = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o.gsec) >> 32);
+#pragma unroll
+  for (int p = 0; p < kWave / 16; ++p) {
+    if (!((any >> (16 * p)) & 0xffffull)) continue;
+    const int src = 16 * p + (lane >> 2);
+    const int sa = src << 2;
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sa, static_cast<int>(glo)));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sa, static_cast<int>(ghi)));
+    const uint32_t ls = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sa, static_cast<int>(o.lds_sec)));
+    if ((any >> src) & 1) {
+      uint8_t *g = reinterpret_cast<uint8_t *>((static_cast<uintptr_t>(hi) << 32) | lo);
+      const uint4 w = lds_u128(ls + 16 * (lane & 3));
+      if (plain) *reinterpret_cast<uint4 *>(g + 16 * (lane & 3)) = w;
+      else store_nt16(g + 16 * (lane & 3), w);
+    }
+  }
+  compiler_barrier();
+}
+
+__device__ __forceinline__ FrameRef lane_ref(const KernelArgs &a, const uint4 d, uint32_t f) {
+  return make_ref(a, (static_cast<uint64_t>(d.y) << 32) | d.x, d.z, f < a.n);
+}
+
+template <int NCH, int SPT>
+__global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs args) {
+  constexpr uint32_t T = SPT * kWave;        // frames per tile
+  __shared__ __attribute__((aligned(16))) uint8_t hdr[kWavesPerBlock][kWave][kLaneSlot];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t slot = lds_addr(&hdr[wv][lane][0]);
+  const uint32_t waves = gridDim.x * kWavesPerBlock;
+  const uint32_t last = args.n - 1;
+  clear_next_count(args);
+
+  uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
+  uint32_t nrec = 0;
+  uint4 dn[SPT];
+#pragma unroll
+  for (int st = 0; st < SPT; ++st)
+    dn[st] = *reinterpret_cast<const uint4 *>(args.descs + min(tile * T + st * kWave + lane, last));
+  for (; tile * T < args.n; tile += waves) {
+    const uint32_t tf0 = tile * T;
+    uint4 d[SPT];
+#pragma unroll
+    for (int st = 0; st < SPT; ++st) {
+      d[st] = dn[st];
+      dn[st] = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * T + st * kWave + lane, last));
+    }
+    uint4 v[2][NCH];
+    FrameRef r[2];
+    r[0] = lane_ref(args, d[0], tf0 + lane);
+    load_lane<NCH>(r[0], v[0]);
+#pragma unroll
+    for (int st = 0; st < SPT; ++st) {
+      // step st: process buffer st & 1, prefetch step st + 1 into the other
+      if (st + 1 < SPT) {
+        r[(st + 1) & 1] = lane_ref(args, d[st + 1], tf0 + (st + 1) * kWave + lane);
+        load_lane<NCH>(r[(st + 1) & 1], v[(st + 1) & 1]);
+      }
+      const LaneOut o = process_lane<NCH>(args, r[st & 1], v[st & 1], slot);
+      store_sectors(o, lane, args.plain_sector);
+      const uint32_t f = tf0 + st * kWave + lane;
+      nrec += store_result(args, f, f < args.n, o.res);
+      compiler_barrier();   // the next frame rewrites this lane's header window
+    }
+  }
+  publish_records(args, nrec, lane);
+}
+
 // ---- LDS-DMA ring kernel ------------------------------------------------------
 //
 // Each wave streams its steps (G frames, one per group) through a private ring
@@ -844,6 +1007,13 @@ int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel launch");
 }
 
+template <int NCH, int SPT>
+int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
+  auto k = checksum_kernel_lane<NCH, SPT>;
+  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, SPT * kWave)), dim3(kBlock), 0, stream, a);
+  return finish_launch(a, stream, "checksum_kernel_lane launch");
+}
+
 template <int LPF, int NCH, int R>
 int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   auto k = checksum_kernel_dma<LPF, NCH, R>;
@@ -859,8 +1029,11 @@ struct Variant {
 };
 
 #define XSKNF_V(L, N, S) {L, N, S, 0, &launch_reg<L, N, S>}
+#define XSKNF_L(N, S) {1, N, S, 0, &launch_lane<N, S>}
 #define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
 const Variant kVariants[] = {
+    XSKNF_L(5, 2),     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
+    XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
     XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 2), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
     XSKNF_V(64, 2, 4), XSKNF_V(64, 2, 8), XSKNF_V(64, 4, 4), XSKNF_V(64, 9, 2), XSKNF_V(64, 9, 4),
@@ -869,6 +1042,7 @@ const Variant kVariants[] = {
     XSKNF_D(64, 4, 2), XSKNF_D(64, 4, 3),
 };
 #undef XSKNF_V
+#undef XSKNF_L
 #undef XSKNF_D
 
 const Variant *find_variant(int lpf, int nch, int u, int ring) {
@@ -883,13 +1057,15 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.blocks_per_cu = 8;
   c.lds_ring = 0;
   // measured best per size class on MI355X (tools/tune.py, 1M-frame batches):
-  // up to ~1 KiB, 8 lanes per frame, every check in-line as a whole-sector
-  // rewrite and no scatter pass (64 B: 60 us vs 77 us with 2-byte stores + the
-  // pass); 1500 B, 16 lanes x 2 chunks with long frames' checks deferred and the
-  // short ones of a mix written as 2 bytes (whole sectors cost IMIX ~10 %);
-  // jumbo frames, one wave per frame
-  if (hint <= 1024) {
-    c.lanes_per_frame = 8; c.chunks_per_lane = 1; c.fused_stores = 1;
+  // frames that fit a 5-chunk window, one lane per frame with 2-byte in-line
+  // checks (64 B: 50 us); up to ~1 KiB, 4 lanes per frame, every check in-line
+  // as a whole-sector rewrite and no scatter pass; 1500 B, 16 lanes x 2 chunks
+  // with long frames' checks deferred and the short ones of a mix written as 2
+  // bytes (whole sectors cost IMIX ~10 %); jumbo frames, one wave per frame
+  if (hint + 15 <= 80) {
+    c.lanes_per_frame = 1; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 5;
+  } else if (hint <= 1024) {
+    c.lanes_per_frame = 4; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1;
   } else if (hint + 15 <= 2048) {
     c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.fused_stores = 4;
   } else if (hint + 15 <= 4096) {
@@ -918,6 +1094,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
   a.defer_min_len = kDeferMinLen;
   a.no_scatter = 0;
   a.sector_stores = 1;
+  a.plain_sector = 0;
   a.seq = 0;
   a.count_records = 0;
   // aligned-down descriptor address: inside the descriptor array's own page
@@ -927,14 +1104,15 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
 
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
-  const int mode = cfg.fused_stores & 3;          // + 4: 2-byte in-line stores
-  if (cfg.fused_stores < 0 || cfg.fused_stores > 7) return -EINVAL;
+  const int mode = cfg.fused_stores & 3;          // + 4: 2-byte in-line stores, + 8: plain sector stores
+  if (cfg.fused_stores < 0 || cfg.fused_stores > 15) return -EINVAL;
   const Variant *v = find_variant(cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group, cfg.lds_ring);
   if (!v) return -EINVAL;
   KernelArgs a = base;
   a.defer_min_len = mode == 1 ? kNoDefer : (mode >= 2 ? 0u : kDeferMinLen);
   if (mode == 3) a.no_scatter = 1;   // records only: the caller applies the checks
   if (cfg.fused_stores & 4) a.sector_stores = 0;
+  if (cfg.fused_stores & 8) a.plain_sector = 1;
   static std::atomic<uint32_t> seq{0};
   a.seq = seq.fetch_add(1, std::memory_order_relaxed);
   a.count_records = a.defer_min_len != kNoDefer && !a.no_scatter;

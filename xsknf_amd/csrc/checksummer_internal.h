@@ -27,6 +27,8 @@ struct KernelArgs {
   uint32_t sector_stores;  // 1: an in-line check whose 64-byte sector lies inside the
                            // frame is written as that whole sector (device memory:
                            // no read-modify-write); 0: 2-byte stores (host memory)
+  uint32_t plain_sector;   // 1: whole-sector stores of the lane kernel are plain (write-back),
+                           // 0: non-temporal
 };
 
 // Check record parked in verdicts[f] by the summing pass (deferred stores):
