@@ -223,6 +223,51 @@ __global__ __launch_bounds__(256) void scatter_rw(uint8_t *__restrict__ base, ui
   }
 }
 
+// read pass (nt, flat pieces) that also parks every chunk's 64-B check sector
+// (the aligned block holding byte off+40) in a compact side buffer: the (up to
+// 4) adjacent lanes holding a sector's pieces store them in one instruction
+__global__ __launch_bounds__(256) void probe_side(const uint8_t *__restrict__ base, uint64_t pieces,
+                                                  uint32_t ppc, uint32_t stride, uint32_t off,
+                                                  uint32_t *__restrict__ out, uint8_t *__restrict__ side) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  uint32_t acc = 0;
+  const uint64_t tid = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t nthr = gridDim.x * 256ull;
+  const uint32_t s0 = ((off + 40) & ~63u) - off;   // sector start, chunk-data relative
+  for (uint64_t i = tid; i < pieces; i += 4 * nthr) {
+    u4v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t j = min(i + k * nthr, pieces - 1);
+      const uint64_t c = j / ppc, p = j % ppc;
+      v[k] = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(base + c * stride + off + p * 16));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+      const uint64_t j = i + k * nthr;
+      const uint64_t c = j / ppc, p = j % ppc;
+      if (j < pieces && p * 16 >= s0 && p * 16 < s0 + 64)
+        __builtin_nontemporal_store(v[k], reinterpret_cast<u4v *>(side + c * 64 + (p * 16 - s0)));
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// write pass from the side buffer: 4 lanes per chunk, nt 16-B load + nt store
+__global__ __launch_bounds__(256) void scatter_side(uint8_t *__restrict__ base, uint64_t chunks,
+                                                    uint32_t stride, uint32_t off,
+                                                    const uint8_t *__restrict__ side) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < chunks * 4; t += gridDim.x * 256ull) {
+    const uint64_t c = t / 4;
+    const int piece = t % 4;
+    uint8_t *sec = base + ((c * stride + off + 40) & ~(uint64_t)63);
+    u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(side + c * 64 + 16 * piece));
+    __builtin_nontemporal_store(v, reinterpret_cast<u4v *>(sec + 16 * piece));
+  }
+}
+
 int main(int argc, char **argv) {
   if (argc < 5) { fprintf(stderr, "usage: %s chunks stride off len [reps]\n", argv[0]); return 2; }
   const uint64_t chunks = strtoull(argv[1], 0, 0);
@@ -336,6 +381,37 @@ int main(int argc, char **argv) {
       printf("{\"head\": %u, \"read_us\": %.2f, \"scatter_rw_us\": %.2f}\n", hd,
              rsum * 1e3 / (reps - 1), ssum * 1e3 / (reps - 1));
     }
+  }
+  if (getenv("PROBE_SIDE")) {
+    // A: nt read pass + scatter_rw (re-read sector, write it back)   [the product today]
+    // B: read pass parking sectors in a side buffer + scatter_side     [no sector re-read]
+    uint8_t *side;
+    CHECK(hipMalloc(&side, chunks * 64));
+    CHECK(hipMemset(side, 0, chunks * 64));
+    for (int mode = 0; mode < 2; ++mode) {
+      double rsum = 0, ssum = 0;
+      for (int r = 0; r < reps; ++r) {
+        hipEvent_t a0, a1, a2;
+        CHECK(hipEventCreate(&a0)); CHECK(hipEventCreate(&a1)); CHECK(hipEventCreate(&a2));
+        CHECK(hipEventRecord(a0));
+        if (mode == 0) hipLaunchKernelGGL(probe_mode<1>, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out);
+        else hipLaunchKernelGGL(probe_side, dim3(grid), dim3(256), 0, 0, buf, pieces, ppc, stride, off, out, side);
+        CHECK(hipEventRecord(a1));
+        if (mode == 0) hipLaunchKernelGGL(scatter_rw, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, verdicts);
+        else hipLaunchKernelGGL(scatter_side, dim3(grid), dim3(256), 0, 0, buf, chunks, stride, off, side);
+        CHECK(hipEventRecord(a2));
+        CHECK(hipEventSynchronize(a2));
+        float t1 = 0, t2 = 0;
+        CHECK(hipEventElapsedTime(&t1, a0, a1));
+        CHECK(hipEventElapsedTime(&t2, a1, a2));
+        if (r > 0) { rsum += t1; ssum += t2; }
+        CHECK(hipEventDestroy(a0)); CHECK(hipEventDestroy(a1)); CHECK(hipEventDestroy(a2));
+      }
+      printf("{\"side_mode\": \"%s\", \"len\": %u, \"read_us\": %.2f, \"scatter_us\": %.2f, \"total_us\": %.2f}\n",
+             mode == 0 ? "reread" : "side", len, rsum * 1e3 / (reps - 1), ssum * 1e3 / (reps - 1),
+             (rsum + ssum) * 1e3 / (reps - 1));
+    }
+    CHECK(hipFree(side));
   }
   if (getenv("PROBE_SCATTER")) {
     CHECK(hipEventRecord(e0));
