@@ -145,6 +145,7 @@ def time_workload(name, args, world, rank, dev, seed):
     cfg = _lib.LaunchCfg()
     _lib.check(lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(cfg)), "default_launch_cfg")
     single_kernel = (cfg.fused_stores & 3) == 1
+    family = "checksum_kernel_split" if cfg.kernel == 1 else "checksum_kernel"
     k_ms = None
     if args.kernel_steps > 0 and not single_kernel:
         cfg.fused_stores = 3
@@ -174,7 +175,7 @@ def time_workload(name, args, world, rank, dev, seed):
     bytes_len = int(lens.sum())
     counters = allreduce_sum_i64([n, bytes_len, int((vh == -1).sum()), int((vh >= 0).sum())], world)
     res = dict(name=name, desc=desc, n=n, lens=lens, bytes_len=bytes_len, kernel_ms=kernel_ms, sum_ms=k_ms,
-               single_kernel=single_kernel,
+               single_kernel=single_kernel, family=family,
                wall_max=wall_max, counters=counters, umem=umem, descs=descs, verdicts=verdicts,
                sample=sample, layout=layout, chunk=chunk)
     return res
@@ -251,9 +252,9 @@ def main():
     if prim["sum_ms"] is not None:
         k_s = prim["sum_ms"] / 1e3
         alg_bytes = prim["bytes_len"] + prim["n"] * (DESC_BYTES + VERDICT_BYTES)
-        kernel = "checksum_kernel (records only, launched alone)"
+        kernel = f"{prim['family']} (records only, launched alone)"
     elif prim["single_kernel"]:
-        k_s, alg_bytes, kernel = step_k_s, step_alg, "checksum_kernel (checks in-line: the whole step)"
+        k_s, alg_bytes, kernel = step_k_s, step_alg, f"{prim['family']} (checks in-line: the whole step)"
     else:
         k_s, alg_bytes, kernel = step_k_s, step_alg, "whole step (summing + scatter)"
     achieved = alg_bytes / k_s / 1e9

@@ -114,11 +114,22 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * In-line checks whose 64-byte sector lies inside the frame are written as
  * that whole sector (group and lane kernels); adding 4 to `fused_stores` writes
  * the 2 check bytes alone instead, adding 8 makes the lane kernel's sector
- * stores plain (write-back) rather than non-temporal (A/B).  Only instantiated shapes are accepted (-EINVAL
+ * stores plain (write-back) rather than non-temporal (A/B).
+ * `kernel` = XSKNF_GPU_KERNEL_SPLIT selects the split kernel (the default for
+ * every hint): lane l of a wave parses, sums and finishes frame l of a
+ * 64-frame tile from its first `window_chunks` & 15 (4..7, or 8) chunks, and the
+ * payload of longer frames is summed in items of one pass of `lanes_per_frame`
+ * x `chunks_per_lane` chunks dealt to the wave's lane groups, `frames_per_group`
+ * items per group in flight (any mix of lengths keeps every lane busy);
+ * `window_chunks` + 16 loads the windows transposed (W lanes per frame, one
+ * coalesced request).  Only instantiated shapes are accepted (-EINVAL
  * otherwise); every shape gives identical results.
  */
 #define XSKNF_GPU_RECORD_TAG 0x40000000u       /* bits 31..30 = 01 */
 #define XSKNF_GPU_RECORD_TAG_MASK 0xC0000000u
+
+#define XSKNF_GPU_KERNEL_AUTO 0    /* group register / lane / LDS-DMA kernel by the fields above */
+#define XSKNF_GPU_KERNEL_SPLIT 1   /* headers by lane, payload by lane groups */
 
 struct xsknf_gpu_launch_cfg {
 	int32_t lanes_per_frame;
@@ -127,6 +138,8 @@ struct xsknf_gpu_launch_cfg {
 	int32_t blocks_per_cu;
 	int32_t lds_ring;
 	int32_t fused_stores;
+	int32_t kernel;          /* XSKNF_GPU_KERNEL_* */
+	int32_t window_chunks;   /* split kernel: header window per lane (16-byte chunks), +16 transposed load */
 };
 
 /* The shape xsknf_gpu_checksum_batch() uses for a given frame_len_hint. */

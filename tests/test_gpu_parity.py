@@ -180,7 +180,20 @@ SHAPES = [
     (1, 5, 2, 0, 1), (1, 5, 4, 0, 0), (1, 6, 2, 0, 9), (1, 7, 2, 0, 5), (1, 5, 2, 0, 2),
     # 2-byte in-line stores instead of whole-sector rewrites
     (8, 1, 4, 0, 5), (16, 2, 4, 0, 4), (32, 3, 4, 0, 5),
+    # split kernel (headers by lane, payload items by lane groups): + kernel, window
+    (16, 2, 2, 0, 0, 1, 4), (16, 2, 1, 0, 1, 1, 4), (8, 4, 2, 0, 2, 1, 4), (32, 1, 2, 0, 5, 1, 4),
+    (16, 4, 1, 0, 4, 1, 4), (16, 2, 2, 0, 0, 1, 5), (64, 2, 1, 0, 0, 1, 4), (32, 2, 1, 0, 1, 1, 4),
+    (16, 2, 1, 0, 0, 1, 7), (16, 3, 1, 0, 2, 1, 4), (8, 2, 2, 0, 1, 1, 4),
+    (16, 2, 2, 0, 0, 1, 20), (16, 3, 1, 0, 1, 1, 20), (16, 2, 1, 0, 5, 1, 20),
+    (16, 3, 1, 0, 0, 1, 24), (16, 2, 2, 0, 1, 1, 24), (32, 3, 1, 0, 2, 1, 24),
 ]
+
+
+def launch_cfg(shape, bpc=4, fused=None):
+    from xsknf_amd import _lib
+    kernel, window = (shape[5], shape[6]) if len(shape) > 5 else (0, 0)
+    return _lib.LaunchCfg(shape[0], shape[1], shape[2], bpc, shape[3], shape[4] if fused is None else fused,
+                          kernel, window)
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=["-".join(map(str, s)) for s in SHAPES])
@@ -201,7 +214,7 @@ def test_every_launch_shape_is_bit_exact(dev, shape, layout):
     umem = torch.from_numpy(b.umem).to(dev)
     descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
     v = torch.empty(b.n, dtype=torch.int32, device=dev)
-    cfg = _lib.LaunchCfg(shape[0], shape[1], shape[2], 4, shape[3], shape[4])
+    cfg = launch_cfg(shape)
     rc = lib.xsknf_gpu_checksum_batch_cfg(
         ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), b.n, 1,
         ctypes.byref(_lib.CsumOpts(2, O.REDIRECT, 3, 0)), ctypes.c_void_p(v.data_ptr()),
@@ -212,7 +225,8 @@ def test_every_launch_shape_is_bit_exact(dev, shape, layout):
     assert np.array_equal(umem.cpu().numpy(), ou)
 
 
-@pytest.mark.parametrize("shape", [(16, 2, 4, 0), (8, 1, 4, 0), (64, 4, 1, 3)], ids=["reg16", "reg8", "dma64"])
+@pytest.mark.parametrize("shape", [(16, 2, 4, 0), (8, 1, 4, 0), (64, 4, 1, 3), (16, 2, 2, 0, 0, 1, 4)],
+                         ids=["reg16", "reg8", "dma64", "split16"])
 def test_records_only_mode(dev, shape):
     """fused_stores = 3: the UMEM is only read; applying the records as
     include/xsknf_gpu.h documents them gives the oracle's bytes and verdicts."""
@@ -225,7 +239,7 @@ def test_records_only_mode(dev, shape):
     umem = torch.from_numpy(b.umem).to(dev)
     descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
     v = torch.empty(b.n, dtype=torch.int32, device=dev)
-    cfg = _lib.LaunchCfg(shape[0], shape[1], shape[2], 4, shape[3], 3)
+    cfg = launch_cfg(shape, fused=3)
     assert lib.xsknf_gpu_checksum_batch_cfg(
         ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), b.n, 1,
         ctypes.byref(_lib.CsumOpts(2, O.REDIRECT, 3, 0)), ctypes.c_void_p(v.data_ptr()),

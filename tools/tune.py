@@ -4,8 +4,9 @@ rounds, median of per-round HIP-event timings), on device-resident batches.
 
     python tools/tune.py --workload 1500 --variants 32,3,2:32,3,1:64,2,1:32,3,1,3 [--bpc 8,4]
 
-A variant is lanes_per_frame,chunks_per_lane,frames_per_group[,lds_ring[,fused_stores]]
-(lds_ring > 0 selects the LDS-DMA kernel; fused_stores 1 = single-pass stores).
+A variant is lanes_per_frame,chunks_per_lane,frames_per_group[,lds_ring[,fused_stores[,kernel,window]]]
+(lds_ring > 0 selects the LDS-DMA kernel; fused_stores 1 = single-pass stores;
+kernel 1 = the split kernel with a `window`-chunk header window per lane).
 
 Every variant's output (verdicts + whole UMEM) is compared with the default
 shape's output, so a tuning run is also a cross-variant parity check.
@@ -50,10 +51,10 @@ def main():
     dflt = _lib.LaunchCfg()
     lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(dflt))
     shapes = [(dflt.lanes_per_frame, dflt.chunks_per_lane, dflt.frames_per_group, dflt.lds_ring,
-               dflt.fused_stores)]
+               dflt.fused_stores, dflt.kernel, dflt.window_chunks)]
     for t in [x for x in a.variants.split(":") if x]:
         s = tuple(int(y) for y in t.split(","))
-        s = s + (0,) * (5 - len(s))
+        s = s + (0,) * (7 - len(s))
         if s not in shapes:
             shapes.append(s)
     bpcs = [int(x) for x in a.bpc.split(",")]
@@ -63,7 +64,7 @@ def main():
     verd = torch.empty(n, dtype=torch.int32, device=dev)
 
     def run(cfg, um, vv):
-        c = _lib.LaunchCfg(cfg[0][0], cfg[0][1], cfg[0][2], cfg[1], cfg[0][3], cfg[0][4])
+        c = _lib.LaunchCfg(cfg[0][0], cfg[0][1], cfg[0][2], cfg[1], cfg[0][3], cfg[0][4], cfg[0][5], cfg[0][6])
         rc = lib.xsknf_gpu_checksum_batch_cfg(ctypes.c_void_p(um.data_ptr()), um.numel(),
                                               ctypes.c_void_p(descs.data_ptr()), n, 0,
                                               ctypes.byref(opts), ctypes.c_void_p(vv.data_ptr()),

@@ -59,6 +59,8 @@ class LaunchCfg(ctypes.Structure):
         ("blocks_per_cu", ctypes.c_int32),
         ("lds_ring", ctypes.c_int32),
         ("fused_stores", ctypes.c_int32),
+        ("kernel", ctypes.c_int32),          # XSKNF_GPU_KERNEL_AUTO 0 / _SPLIT 1
+        ("window_chunks", ctypes.c_int32),   # split kernel header window
     ]
 
 

@@ -23,9 +23,13 @@
 // * Waves own TILES of 64 consecutive frames (persistent grid striding over
 //   tiles), so per-frame results collect in LDS and leave as one 256-B store.
 // * Loads are non-temporal (streamed once; +8-10 % read bandwidth measured).
-// * Two kernel families, same results:
+// * Kernel families, same results:
+//     - split (the default): lane l of a wave parses / finishes frame l of a
+//       64-frame tile from its header window, and the payload past the window
+//       is summed in one-pass items dealt to lane groups (any mix of lengths);
 //     - register: each step loads U frames per group into VGPRs, then parses /
 //       sums / reduces them one by one (frame u+1 in flight behind frame u);
+//     - lane: one lane per frame, whole frame (small frames);
 //     - LDS-DMA ring: each wave streams frames through R LDS slots filled by
 //       global_load_lds_dwordx4; R-1 steps stay in flight at no VGPR cost.
 // * Group partial sums reduce with DPP (row_shr / row_bcast) into the group's
@@ -718,6 +722,360 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs 
   publish_records(args, nrec, lane);
 }
 
+// ---- split kernel: headers by lane, payload by group ----------------------------
+//
+// The group kernels pay a frame's fixed work (descriptor, header parse, verdict,
+// check store) once per GROUP: LPF lanes redo it, and a short frame leaves most
+// of its group idle.  With a mix of lengths (IMIX) or medium frames (570 B)
+// that overhead, not HBM, sets the time.  Here a wave takes a tile of 64
+// consecutive frames in three phases:
+//  A. lane l owns frame l: it loads the frame's first W chunks (the header
+//     window), parses the header in its LDS slot, sums the window and, when the
+//     frame fits the window, finishes it exactly as the lane kernel does;
+//  B. the payload of the longer frames past the window is cut into ITEMS of one
+//     group pass (LPF lanes x NCH chunks) and the items are dealt to the wave's
+//     groups round robin, so the groups stay balanced whatever the mix; item
+//     sums meet in a per-frame LDS accumulator (ds_add);
+//  C. lane l folds its frame's total and stores the check (2 bytes in-line, or
+//     a record for the scatter pass).
+// The item list reuses the lane slots (dead after phase A).  Frames with more
+// items than a slot share holds take a whole-wave loop (correctness path).
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_t &total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), o, kWave));
+    if (lane >= o) x += y;
+  }
+  total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), kWave - 1));
+  return x - v;
+}
+
+__device__ __forceinline__ void lds_add_u32(uint32_t a, uint32_t v) {
+  __hip_atomic_fetch_add(reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(static_cast<uintptr_t>(a)),
+                         v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+__device__ __forceinline__ void lds_store_u16(uint32_t a, uint16_t v) {
+  *reinterpret_cast<__attribute__((address_space(3))) uint16_t *>(static_cast<uintptr_t>(a)) = v;
+}
+
+__device__ __forceinline__ uint32_t lds_u16(uint32_t a) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint16_t *>(static_cast<uintptr_t>(a));
+}
+
+__device__ __forceinline__ uint32_t lds_byte(uint32_t a) {
+  return *reinterpret_cast<const lds_u8 *>(static_cast<uintptr_t>(a));
+}
+
+// Frame bytes rebuilt from integers (LDS) must be marked global, or hipcc
+// emits FLAT loads, which count in lgkmcnt too and serialize every LDS read
+// behind the loads in flight.
+typedef const __attribute__((address_space(1))) u32x4 *gchunk_ptr;
+
+__device__ __forceinline__ uint4 load_nt(gchunk_ptr p) {
+  const u32x4 x = __builtin_nontemporal_load(p);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+// A payload frame as phase B sees it: {fp lo, fp hi, len, u} in LDS.
+struct Payload {
+  gchunk_ptr cp;
+  int nch, lo, hi;
+  uint32_t wl, wh;
+};
+
+__device__ __forceinline__ Payload payload_of(uint4 m) {
+  Payload p;
+  const uintptr_t fp = (static_cast<uintptr_t>(m.y) << 32) | m.x;
+  const int rs = static_cast<int>(fp & 15);
+  p.cp = reinterpret_cast<gchunk_ptr>(fp - rs);
+  p.nch = static_cast<int>((static_cast<uint64_t>(rs) + m.z + 15) >> 4);
+  p.lo = rs + static_cast<int>(m.w);
+  p.hi = rs + static_cast<int>(m.z);
+  p.wl = (p.lo & 1) ? 0x01000100u : 0x00010001u;
+  p.wh = p.wl << 8 | p.wl >> 24;
+  return p;
+}
+
+// Phase B's loads are issued from inline asm with explicitly counted waits:
+// hipcc drains vmcnt to 0 at the top of any loop whose loads are consumed in a
+// later iteration, which would serialize the two-stage pipeline.  Each loaded
+// register is bound to its wait (an empty asm with a "+v" operand after the
+// s_waitcnt), so no use can move above the wait, and a stage that is never
+// consumed is drained before its registers can be reused.
+__device__ __forceinline__ u32x4 gload_nt_asm(gchunk_ptr p) {
+  u32x4 x;
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(x) : "v"(p) : "memory");
+  return x;
+}
+
+// One stage of phase B: U items per group, NCH chunks per lane each.
+template <int U, int NCH>
+struct ItemStage {
+  u32x4 t[U][NCH];
+  Payload pl[U];
+  uint32_t fi[U];
+  int c0[U];
+  bool ok[U];
+
+  template <int W, int LPF, int SPAN>
+  __device__ __forceinline__ void issue(uint32_t area, uint32_t mt, uint32_t it0, uint32_t total, int grp, int gl) {
+    constexpr int G = kWave / LPF;
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const uint32_t it = it0 + q * G + grp;
+      ok[q] = it < total;
+      const uint32_t e = lds_u16(area + 2 * min(it, total - 1));
+      fi[q] = e >> 8;
+      pl[q] = payload_of(lds_u128(mt + 16 * fi[q]));
+      c0[q] = W + static_cast<int>(e & 0xff) * SPAN;
+      if (!ok[q]) pl[q].hi = pl[q].lo;   // masked: sums nothing
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q)
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) t[q][k] = gload_nt_asm(pl[q].cp + min(c0[q] + k * LPF + gl, pl[q].nch - 1));
+  }
+
+  // wait until at most N vector-memory operations younger than this stage's are outstanding
+  template <int N>
+  __device__ __forceinline__ void wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx950");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+    for (int q = 0; q < U; ++q)
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) asm volatile("" : "+v"(t[q][k]));
+  }
+
+  template <int LPF>
+  __device__ __forceinline__ void consume(uint32_t ab, int gl) {
+    wait<U * NCH>();   // the other stage's loads stay in flight
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      uint32_t blo = 0, bhi = 0;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const uint4 v = make_uint4(t[q][k].x, t[q][k].y, t[q][k].z, t[q][k].w);
+        chunk_sum_fast(v, (c0[q] + k * LPF + gl) * 16, pl[q].lo, pl[q].hi, pl[q].wl, pl[q].wh, blo, bhi);
+      }
+      const uint32_t P = group_sum_last<LPF>(blo + (bhi << 8));
+      if (gl == LPF - 1 && ok[q]) lds_add_u32(ab + 4 * fi[q], P);
+    }
+  }
+};
+
+template <int W, int LPF, int NCH, int U, bool TL>
+__global__ __launch_bounds__(kBlock) void checksum_kernel_split(const KernelArgs args) {
+  static_assert(W >= 4 && (W <= kHdrChunks || W == 8), "header window");
+  static_assert(!TL || W == 4 || W == 8, "transposed window load: W lanes x 16 B per frame");
+  static_assert(kWave % LPF == 0 && LPF >= 4, "group shape");
+  constexpr int G = kWave / LPF;
+  constexpr int SPAN = LPF * NCH;                          // chunks per item
+  constexpr int kSlot = 16 * W > kLaneSlot ? 16 * W : kLaneSlot;   // per-lane header window
+  constexpr int kSlotArea = kWave * kSlot;                 // bytes per wave
+  constexpr int kItemsPerFrame = kSlotArea / 2 / kWave;    // u16 items: 56 (W <= 7) / 64
+  __shared__ __attribute__((aligned(16))) uint8_t slots[kWavesPerBlock][kSlotArea];
+  __shared__ __attribute__((aligned(16))) uint4 meta[kWavesPerBlock][kWave];
+  __shared__ __attribute__((aligned(16))) uint32_t accb[kWavesPerBlock][kWave];
+
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int grp = lane / LPF, gl = lane % LPF;
+  const uint32_t area = lds_addr(&slots[wv][0]);
+  const uint32_t slot = area + kSlot * lane;
+  const uint32_t mt = lds_addr(&meta[wv][0]);
+  const uint32_t ab = lds_addr(&accb[wv][0]);
+  const uint32_t waves = gridDim.x * kWavesPerBlock;
+  const uint32_t last = args.n - 1;
+  clear_next_count(args);
+
+  uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
+  uint32_t nrec = 0;
+  // descriptors travel two tiles ahead
+  uint4 d = *reinterpret_cast<const uint4 *>(args.descs + min(tile * kWave + lane, last));
+  uint4 dn = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * kWave + lane, last));
+  for (; tile * kWave < args.n; tile += waves) {
+    const uint32_t f = tile * kWave + lane;
+    const FrameRef r = lane_ref(args, d, f);
+    uint4 v[W];
+    if constexpr (TL) {
+      // transposed: lanes W*i .. W*i+W-1 load the window of frame (64/W)*p + i
+      // (p = 0..W-1), one coalesced 16*W-byte request per frame instead of W
+      // 16-byte ones, and drop it in that frame's slot
+      constexpr int FPI = kWave / W;   // frames per load instruction
+      const uintptr_t cpv = reinterpret_cast<uintptr_t>(r.cp);
+      u32x4 x[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int g = FPI * p + lane / W;
+        const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv)));
+        const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
+        const int nc = __builtin_amdgcn_ds_bpermute(g << 2, r.nch);
+        const gchunk_ptr cp = reinterpret_cast<gchunk_ptr>((static_cast<uintptr_t>(hi) << 32) | lo);
+        x[p] = cp[min(lane % W, nc - 1)];
+      }
+      compiler_barrier();
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        lds_store_u128(area + kSlot * (FPI * p + lane / W) + 16 * (lane % W), make_uint4(x[p].x, x[p].y, x[p].z, x[p].w));
+      compiler_barrier();
+#pragma unroll
+      for (int k = 0; k < W; ++k) v[k] = lds_u128(slot + 16 * k);
+    } else {
+      load_lane<W>(r, v);
+    }
+    const uint4 dnn = *reinterpret_cast<const uint4 *>(args.descs + min((tile + 2 * waves) * kWave + lane, last));
+    // per-tile store policy, as the register kernel: long frames defer their
+    // checks only where they are at least half of the tile
+    uint32_t defer_min = args.defer_min_len;
+    if (defer_min != kNoDefer && defer_min != 0 && !args.no_scatter) {
+      const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
+          __builtin_amdgcn_ballot_w64(f < args.n && d.z >= defer_min)));
+      const uint32_t nlive = min(static_cast<uint32_t>(kWave), args.n - tile * kWave);
+      if (2 * nlong < nlive) defer_min = kNoDefer;
+    }
+
+    // ---- phase A: header, window sum, short frames finished ----
+    compiler_barrier();
+    if constexpr (!TL) {
+#pragma unroll
+      for (int k = 0; k < W; ++k) lds_store_u128(slot + 16 * k, v[k]);
+    }
+    compiler_barrier();
+    {  // header bytes past the window (large ihl, or a frame start late in its chunk)
+      const int u0 = 14 + 4 * static_cast<int>(lds_byte(slot + r.rs + 14) & 0x0f);
+      const int need = min((r.rs + u0 + 8 + 15) >> 4, r.nch);
+      for (int k = W; k < need; ++k) lds_store_u128(slot + 16 * k, r.cp[k]);
+    }
+    compiler_barrier();
+    const Header h = parse_header(slot + r.rs);
+    compiler_barrier();
+    bool do_sum;
+    const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
+    const int lo = r.rs + h.u, hi = r.rs + r.len;
+    const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+    const uint32_t wh = wl << 8 | wl >> 24;
+    uint32_t acc_lo = 0, acc_hi = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) chunk_sum(v[k], 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
+    const uint32_t PA = acc_lo + (acc_hi << 8);
+    const bool more = do_sum && r.nch > W && args.payload_mult != 0;   // payload past the window
+    const uint32_t items = more ? static_cast<uint32_t>((r.nch - W + SPAN - 1) / SPAN) : 0u;
+    const bool huge = items > static_cast<uint32_t>(kItemsPerFrame);
+    int32_t res = r.exists ? verdict : 0;
+    LaneOut o = {res, false, slot, r.fp};
+    if (do_sum && !more) {
+      const uint16_t c = check_of(h, PA, args.payload_mult);
+      if (static_cast<uint32_t>(r.len) >= defer_min) {
+        res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
+      } else {
+        const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
+        const uintptr_t ck = f0 + h.u + 6;
+        const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
+        const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
+        if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
+            sec + 64 <= c0 + 16 * W) {
+          const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
+          lds_store_u8(at, static_cast<uint8_t>(c));
+          lds_store_u8(at + 1, static_cast<uint8_t>(c >> 8));
+          o.sector = true;
+          o.lds_sec = slot + static_cast<uint32_t>(sec - c0);
+          o.gsec = r.fp + static_cast<intptr_t>(sec - f0);
+        } else {
+          *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+        }
+      }
+    }
+    store_sectors(o, lane, args.plain_sector);
+    const uint32_t part = h.pseudo + args.payload_mult * (PA - h.old_check);
+
+    // ---- phase B: payload items of the longer frames ----
+    if (__builtin_amdgcn_ballot_w64(more)) {
+      const uintptr_t fpv = reinterpret_cast<uintptr_t>(r.fp);
+      lds_store_u128(mt + 16 * lane, make_uint4(static_cast<uint32_t>(fpv), static_cast<uint32_t>(fpv >> 32),
+                                                static_cast<uint32_t>(r.len), static_cast<uint32_t>(h.u)));
+      lds_store_u32(ab + 4 * lane, 0u);
+      uint32_t total;
+      const uint32_t mine = huge ? 0u : items;
+      const uint32_t start = wave_excl_scan(mine, lane, total);
+      compiler_barrier();   // the item list overwrites the (consumed) lane slots
+      for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < mine); ++k)
+        if (k < mine) lds_store_u16(area + 2 * (start + k), static_cast<uint16_t>((lane << 8) | k));
+      compiler_barrier();
+      // two stages of U items per group, ping-pong: the loads of stage s+1 are in
+      // flight while stage s is summed (a stage past the list reloads the last
+      // item, masked: straight-line code keeps vmcnt counted, not drained)
+      if (total) {
+        ItemStage<U, NCH> sa, sb;
+        sa.template issue<W, LPF, SPAN>(area, mt, 0, total, grp, gl);
+        for (uint32_t it0 = 0;;) {
+          sb.template issue<W, LPF, SPAN>(area, mt, it0 + G * U, total, grp, gl);
+          sa.template consume<LPF>(ab, gl);
+          if ((it0 += G * U) >= total) { sb.template wait<0>(); break; }
+          sa.template issue<W, LPF, SPAN>(area, mt, it0 + G * U, total, grp, gl);
+          sb.template consume<LPF>(ab, gl);
+          if ((it0 += G * U) >= total) { sa.template wait<0>(); break; }
+        }
+      }
+      // frames past the item budget: the whole wave sums each one
+      for (uint64_t hm = __builtin_amdgcn_ballot_w64(huge); hm; hm &= hm - 1) {
+        const int fl = __builtin_ctzll(hm);
+        const Payload pl = payload_of(lds_u128(mt + 16 * fl));
+        uint32_t blo = 0, bhi = 0;
+        for (int c = W + lane; __builtin_amdgcn_ballot_w64(c < pl.nch); c += kWave)
+          chunk_sum_fast(load_nt(pl.cp + min(c, pl.nch - 1)), c * 16, pl.lo, pl.hi, pl.wl, pl.wh, blo, bhi);
+        const uint32_t P = group_sum_last<kWave>(blo + (bhi << 8));
+        if (lane == kWave - 1) lds_add_u32(ab + 4 * fl, P);
+      }
+      compiler_barrier();
+      // ---- phase C: fold, check, store ----
+      // an in-line check whose 64-byte sector lies in the frame and the window
+      // is written as that whole sector, patched in the window registers and
+      // staged in the (now free) slot area for the wave's coalesced store
+      LaneOut oc = {0, false, area + 64 * lane, r.fp};
+      if (more) {
+        const uint32_t s = part + args.payload_mult * lds_i32(ab + 4 * lane);   // :92-103
+        const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));
+        const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
+        const uintptr_t ck = f0 + h.u + 6;
+        const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
+        const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
+        if (static_cast<uint32_t>(r.len) >= defer_min) {
+          res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
+        } else if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
+                   sec + 64 <= c0 + 16 * W) {
+          const int o = static_cast<int>(ck - c0);          // check offset in the window
+          const int j0 = static_cast<int>(sec - c0) >> 4;   // sector's first window chunk
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            uint4 x = v[0];
+#pragma unroll
+            for (int k = 1; k < W; ++k)
+              if (k == j0 + i) x = v[k];
+            x = put_byte(x, o - 16 * (j0 + i), c);
+            x = put_byte(x, o + 1 - 16 * (j0 + i), c >> 8);
+            lds_store_u128(oc.lds_sec + 16 * i, x);
+          }
+          oc.sector = true;
+          oc.gsec = r.fp + static_cast<intptr_t>(sec - f0);
+        } else {
+          *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+        }
+      }
+      store_sectors(oc, lane, args.plain_sector);
+      compiler_barrier();
+    }
+    nrec += store_result(args, f, f < args.n, res);
+    compiler_barrier();   // the next tile rewrites the slots
+    d = dn;
+    dn = dnn;
+  }
+  publish_records(args, nrec, lane);
+}
+
 // ---- LDS-DMA ring kernel ------------------------------------------------------
 //
 // Each wave streams its steps (G frames, one per group) through a private ring
@@ -885,14 +1243,54 @@ __device__ __forceinline__ void rewrite_check(const KernelArgs &args, uint32_t f
 }
 
 // Dense records (>= 1/4 of the frames): 4 lanes per frame over the whole grid;
-// each lane's record and descriptor loads are independent of any scan.
+// each lane's record and descriptor loads are independent of any scan.  A lane
+// takes kScatterU frames per round, so each round costs two dependent memory
+// round trips (record + descriptor, then the sector) for kScatterU frames
+// rather than per frame: the pass is latency-bound, not bandwidth-bound.
+constexpr int kScatterU = 4;
+
 __device__ __forceinline__ void scatter_dense(const KernelArgs &args) {
   const uint32_t nthreads = gridDim.x * kBlock;
-  for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < 4 * args.n; t += nthreads) {
-    const uint32_t f = t >> 2;
-    const uint32_t r = static_cast<uint32_t>(args.verdicts[f]);
-    const xsknf_gpu_desc d = args.descs[f];
-    if ((r & kRecTagMask) == kRecTag) rewrite_check(args, f, r, d, t & 3);
+  const uint32_t total = 4 * args.n;
+  for (uint32_t t0 = blockIdx.x * kBlock + threadIdx.x; t0 < total; t0 += kScatterU * nthreads) {
+    uint32_t r[kScatterU];
+    xsknf_gpu_desc d[kScatterU];
+#pragma unroll
+    for (int k = 0; k < kScatterU; ++k) {
+      const uint32_t f = min(t0 + k * nthreads, total - 1) >> 2;
+      r[k] = static_cast<uint32_t>(args.verdicts[f]);
+      d[k] = args.descs[f];
+    }
+    uint4 v[kScatterU];
+    uint8_t *mine[kScatterU];
+    int o[kScatterU];
+    bool whole[kScatterU], rec[kScatterU];
+#pragma unroll
+    for (int k = 0; k < kScatterU; ++k) {
+      const uint32_t t = t0 + k * nthreads;
+      rec[k] = t < total && (r[k] & kRecTagMask) == kRecTag;
+      uint8_t *fp = args.umem + umem_offset(d[k].addr);
+      uint8_t *chk = fp + ((r[k] >> 16) & 0x7f) + 6;
+      uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);   // keeps global addressing
+      whole[k] = rec[k] && sec >= fp && sec + 64 <= fp + d[k].len && (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
+      mine[k] = whole[k] ? sec + 16 * (t & 3) : chk;
+      o[k] = static_cast<int>(chk - mine[k]);
+      if (whole[k]) v[k] = load_nt(reinterpret_cast<const uint4 *>(mine[k]));
+    }
+#pragma unroll
+    for (int k = 0; k < kScatterU; ++k) {
+      const uint32_t t = t0 + k * nthreads;
+      const uint16_t c = static_cast<uint16_t>(r[k]);
+      if (whole[k]) {
+        uint4 w = put_byte(v[k], o[k], c);
+        w = put_byte(w, o[k] + 1, c >> 8);
+        store_nt16(mine[k], w);
+      } else if (rec[k] && (t & 3) == 0) {
+        mine[k][0] = static_cast<uint8_t>(c);
+        mine[k][1] = static_cast<uint8_t>(c >> 8);
+      }
+      if (rec[k] && (t & 3) == 0) args.verdicts[t >> 2] = args.fwd_verdict;
+    }
   }
 }
 
@@ -1014,6 +1412,13 @@ int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
 
+template <int W, int LPF, int NCH, int U, bool TL>
+int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
+  auto k = checksum_kernel_split<W, LPF, NCH, U, TL>;
+  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave)), dim3(kBlock), 0, stream, a);
+  return finish_launch(a, stream, "checksum_kernel_split launch");
+}
+
 template <int LPF, int NCH, int R>
 int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   auto k = checksum_kernel_dma<LPF, NCH, R>;
@@ -1022,16 +1427,26 @@ int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
 }
 
 // Instantiated launch shapes: {lanes per frame, 16-B chunks per lane and pass,
-// frames per group and step (register), LDS ring slots (0 = register kernel)}.
+// frames per group and step (register) / items per group in flight (split),
+// LDS ring slots (0 = register kernel), kernel family, header window chunks}.
 struct Variant {
   int lpf, nch, u, ring;
   int (*fn)(const KernelArgs &, hipStream_t, int);
+  int kernel = XSKNF_GPU_KERNEL_AUTO, window = 0;
 };
 
 #define XSKNF_V(L, N, S) {L, N, S, 0, &launch_reg<L, N, S>}
 #define XSKNF_L(N, S) {1, N, S, 0, &launch_lane<N, S>}
 #define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
+// split: window field = W, + 16 for the transposed (coalesced) window load
+#define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
 const Variant kVariants[] = {
+    XSKNF_S(4, 16, 2, 2, 0), XSKNF_S(4, 16, 2, 1, 0), XSKNF_S(4, 8, 4, 2, 0), XSKNF_S(4, 32, 1, 2, 0),
+    XSKNF_S(4, 16, 4, 1, 0), XSKNF_S(5, 16, 2, 2, 0), XSKNF_S(4, 64, 2, 1, 0), XSKNF_S(4, 32, 2, 1, 0),
+    XSKNF_S(7, 16, 2, 1, 0), XSKNF_S(4, 16, 3, 1, 0), XSKNF_S(4, 8, 2, 2, 0),
+    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
+    XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 16, 6, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
+    XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 32, 3, 1, 1),
     XSKNF_L(5, 2),     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
@@ -1044,10 +1459,20 @@ const Variant kVariants[] = {
 #undef XSKNF_V
 #undef XSKNF_L
 #undef XSKNF_D
+#undef XSKNF_S
 
-const Variant *find_variant(int lpf, int nch, int u, int ring) {
-  for (const Variant &v : kVariants)
-    if (v.lpf == lpf && v.nch == nch && v.ring == ring && (ring || v.u == u)) return &v;
+const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
+  for (const Variant &v : kVariants) {
+    if (v.kernel != c.kernel) continue;
+    if (v.kernel == XSKNF_GPU_KERNEL_SPLIT) {
+      if (v.lpf == c.lanes_per_frame && v.nch == c.chunks_per_lane && v.u == c.frames_per_group &&
+          v.window == c.window_chunks)
+        return &v;
+    } else if (v.lpf == c.lanes_per_frame && v.nch == c.chunks_per_lane && v.ring == c.lds_ring &&
+               (c.lds_ring || v.u == c.frames_per_group)) {
+      return &v;
+    }
+  }
   return nullptr;
 }
 
@@ -1057,21 +1482,27 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.blocks_per_cu = 8;
   c.lds_ring = 0;
   // measured best per size class on MI355X (tools/tune.py, 1M-frame batches):
-  // frames that fit a 5-chunk window, one lane per frame with 2-byte in-line
-  // checks (64 B: 50 us); up to ~1 KiB, 4 lanes per frame, every check in-line
-  // as a whole-sector rewrite and no scatter pass; 1500 B, 16 lanes x 2 chunks
-  // with long frames' checks deferred and the short ones of a mix written as 2
-  // bytes (whole sectors cost IMIX ~10 %); jumbo frames, one wave per frame
-  if (hint + 15 <= 80) {
-    c.lanes_per_frame = 1; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 5;
-  } else if (hint <= 1024) {
-    c.lanes_per_frame = 4; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1;
-  } else if (hint + 15 <= 2048) {
-    c.lanes_per_frame = 16; c.chunks_per_lane = 2; c.fused_stores = 4;
+  // the split kernel with the transposed (coalesced) header-window load for
+  // every size class (group kernels in brackets).
+  //  * hint <= 128: 4-chunk window, 16 x 2 items, every check in-line (short
+  //    frames as whole 64-byte sectors), no scatter launch: 64 B 40 us [50];
+  //  * < 1 KiB: 8-chunk window (the frame's whole first 128-byte line, so
+  //    phase B never refetches it): 570 B 144 us [175];
+  //  * < 4 KiB: 8-chunk window, 16 x 3 items, the per-tile policy defers the
+  //    checks of tiles made mostly of long frames (a uniform 1500 B batch) to
+  //    the scatter pass: 1500 B 291 us [305], IMIX 107 us [186];
+  //  * jumbo: 4-chunk window, 16 x 3 items, two per group in flight: 9000 B
+  //    1454 us [1540].
+  c.kernel = XSKNF_GPU_KERNEL_SPLIT;
+  c.lanes_per_frame = 16;
+  if (hint <= 128) {
+    c.window_chunks = 4 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1;
+  } else if (hint < kDeferMinLen) {
+    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1;
   } else if (hint + 15 <= 4096) {
-    c.lanes_per_frame = 64; c.chunks_per_lane = 4; c.fused_stores = 4;
+    c.window_chunks = 8 + 16; c.chunks_per_lane = 3; c.frames_per_group = 1; c.fused_stores = 0;
   } else {
-    c.lanes_per_frame = 64; c.chunks_per_lane = 9; c.fused_stores = 4;
+    c.window_chunks = 4 + 16; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
   }
 }
 
@@ -1106,7 +1537,7 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
   const int mode = cfg.fused_stores & 3;          // + 4: 2-byte in-line stores, + 8: plain sector stores
   if (cfg.fused_stores < 0 || cfg.fused_stores > 15) return -EINVAL;
-  const Variant *v = find_variant(cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group, cfg.lds_ring);
+  const Variant *v = find_variant(cfg);
   if (!v) return -EINVAL;
   KernelArgs a = base;
   a.defer_min_len = mode == 1 ? kNoDefer : (mode >= 2 ? 0u : kDeferMinLen);
