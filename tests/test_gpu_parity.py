@@ -280,3 +280,31 @@ def test_host_path_bit_exact(dev, path, layout):
     assert st["frames"] == b.n
     assert np.array_equal(v, ov)
     assert np.array_equal(umem, ou)
+
+
+@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 1, 1, 20), (16, 3, 1, 0, 0, 1, 24), (16, 3, 2, 0, 2, 1, 20),
+                                   (16, 2, 1, 0, 5, 1, 4)], ids=["w4-16x2", "w8-16x3", "w4-16x3u2", "w4-lane"])
+def test_huge_frames_take_the_whole_wave_path(dev, shape):
+    """Frames with more payload items than the split kernel's per-frame item
+    budget (over ~27-43 KB) are summed by the whole wave; mixed in the same
+    tiles with short and ordinary frames, and with frames past 64 KB."""
+    import ctypes
+    from xsknf_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(5)
+    n = 300
+    lens = np.where(rng.random(n) < 0.3, rng.integers(30000, 200000, size=n),
+                    rng.integers(0, 2000, size=n)).astype(np.uint32)
+    b = frames.unaligned_batch(n, lens, seed=5)
+    frames.inject_edge_cases(b, 0.05)
+    ou, ov = run_oracle(b, iters=3, action=O.REDIRECT, nif=2, ingress=0)
+    umem = torch.from_numpy(b.umem).to(dev)
+    descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+    v = torch.empty(n, dtype=torch.int32, device=dev)
+    assert lib.xsknf_gpu_checksum_batch_cfg(
+        ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), n, 0,
+        ctypes.byref(_lib.CsumOpts(3, O.REDIRECT, 2, 0)), ctypes.c_void_p(v.data_ptr()),
+        ctypes.byref(launch_cfg(shape)), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), ov)
+    assert np.array_equal(umem.cpu().numpy(), ou)
