@@ -393,12 +393,13 @@ __device__ __forceinline__ void finish_long_frames(const KernelArgs &a, uint32_t
 }
 
 // Records per launch, for the scatter pass to pick its shape (per device: a
-// __device__ variable exists once per GPU).  Launch `seq` adds to set seq % 8
-// and clears set (seq + 4) % 8 for a later launch.  A set is 64 counters on
+// __device__ variable exists once per GPU).  Launch `seq` adds to set
+// seq % kCountSlots and clears set (seq + kCountSlots / 2) % kCountSlots for a
+// later launch.  A set is 64 counters on
 // separate 64-byte lines (block b adds to counter b % 64): one shared address
 // would serialize every tile's atomic in one L2 channel.  Only speed depends on
 // the count: both scatter shapes are exact at any record density.
-constexpr uint32_t kCountSlots = 8;
+constexpr uint32_t kCountSlots = 64;
 constexpr uint32_t kCountLanes = 64;
 constexpr uint32_t kCountStride = 16;          // u32 words = 64 bytes
 __device__ uint32_t g_rec_count[kCountSlots][kCountLanes][kCountStride];
@@ -420,7 +421,7 @@ __device__ __forceinline__ void publish_records(const KernelArgs &a, uint32_t nr
 
 __device__ __forceinline__ void clear_next_count(const KernelArgs &a) {
   if (a.count_records && blockIdx.x == 0 && threadIdx.x < kCountLanes)
-    g_rec_count[(a.seq + 4) % kCountSlots][threadIdx.x][0] = 0;
+    g_rec_count[(a.seq + kCountSlots / 2) % kCountSlots][threadIdx.x][0] = 0;
 }
 
 // The launch's record count, on every lane (wave-wide sum of the 64 counters).
@@ -867,8 +868,12 @@ struct ItemStage {
   }
 };
 
+// One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
+// which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
+// +8-11 % from 2 -> 3 waves per SIMD, so the register budget is pinned.
 template <int W, int LPF, int NCH, int U, bool TL>
-__global__ __launch_bounds__(kBlock) void checksum_kernel_split(const KernelArgs args) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U == 1 ? 4 : 1)))
+void checksum_kernel_split(const KernelArgs args) {
   static_assert(W >= 4 && (W <= kHdrChunks || W == 8), "header window");
   static_assert(!TL || W == 4 || W == 8, "transposed window load: W lanes x 16 B per frame");
   static_assert(kWave % LPF == 0 && LPF >= 4, "group shape");
@@ -876,8 +881,10 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_split(const KernelArgs
   constexpr int SPAN = LPF * NCH;                          // chunks per item
   constexpr int kSlot = 16 * W > kLaneSlot ? 16 * W : kLaneSlot;   // per-lane header window
   constexpr int kSlotArea = kWave * kSlot;                 // bytes per wave
-  constexpr int kItemsPerFrame = kSlotArea / 2 / kWave;    // u16 items: 56 (W <= 7) / 64
+  constexpr int kItemCap = 256;                            // items per round of phase B
+  constexpr uint32_t kItemsPerFrame = 255;                 // u8 pass index; more: whole-wave loop
   __shared__ __attribute__((aligned(16))) uint8_t slots[kWavesPerBlock][kSlotArea];
+  __shared__ __attribute__((aligned(16))) uint16_t itemq[kWavesPerBlock][kItemCap];
   __shared__ __attribute__((aligned(16))) uint4 meta[kWavesPerBlock][kWave];
   __shared__ __attribute__((aligned(16))) uint32_t accb[kWavesPerBlock][kWave];
 
@@ -888,6 +895,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_split(const KernelArgs
   const uint32_t slot = area + kSlot * lane;
   const uint32_t mt = lds_addr(&meta[wv][0]);
   const uint32_t ab = lds_addr(&accb[wv][0]);
+  const uint32_t iq = lds_addr(&itemq[wv][0]);
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t last = args.n - 1;
   clear_next_count(args);
@@ -964,7 +972,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_split(const KernelArgs
     const uint32_t PA = acc_lo + (acc_hi << 8);
     const bool more = do_sum && r.nch > W && args.payload_mult != 0;   // payload past the window
     const uint32_t items = more ? static_cast<uint32_t>((r.nch - W + SPAN - 1) / SPAN) : 0u;
-    const bool huge = items > static_cast<uint32_t>(kItemsPerFrame);
+    const bool huge = items > kItemsPerFrame;
     int32_t res = r.exists ? verdict : 0;
     LaneOut o = {res, false, slot, r.fp};
     if (do_sum && !more) {
@@ -1001,23 +1009,27 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_split(const KernelArgs
       uint32_t total;
       const uint32_t mine = huge ? 0u : items;
       const uint32_t start = wave_excl_scan(mine, lane, total);
-      compiler_barrier();   // the item list overwrites the (consumed) lane slots
-      for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < mine); ++k)
-        if (k < mine) lds_store_u16(area + 2 * (start + k), static_cast<uint16_t>((lane << 8) | k));
-      compiler_barrier();
-      // two stages of U items per group, ping-pong: the loads of stage s+1 are in
-      // flight while stage s is summed (a stage past the list reloads the last
-      // item, masked: straight-line code keeps vmcnt counted, not drained)
-      if (total) {
+      // the wave's item list, in rounds of kItemCap: two stages of U items per
+      // group, ping-pong, so the loads of stage s+1 are in flight while stage s
+      // is summed (a stage past the list reloads the last item, masked:
+      // straight-line code keeps vmcnt counted, not drained)
+      for (uint32_t r0 = 0; r0 < total; r0 += kItemCap) {
+        const uint32_t nr = min(total - r0, static_cast<uint32_t>(kItemCap));
+        const uint32_t k0 = r0 > start ? r0 - start : 0u;
+        const uint32_t k1 = r0 + nr > start ? min(mine, r0 + nr - start) : 0u;
+        compiler_barrier();   // the previous round's list has been consumed
+        for (uint32_t k = k0; __builtin_amdgcn_ballot_w64(k < k1); ++k)
+          if (k < k1) lds_store_u16(iq + 2 * (start + k - r0), static_cast<uint16_t>((lane << 8) | k));
+        compiler_barrier();
         ItemStage<U, NCH> sa, sb;
-        sa.template issue<W, LPF, SPAN>(area, mt, 0, total, grp, gl);
+        sa.template issue<W, LPF, SPAN>(iq, mt, 0, nr, grp, gl);
         for (uint32_t it0 = 0;;) {
-          sb.template issue<W, LPF, SPAN>(area, mt, it0 + G * U, total, grp, gl);
+          sb.template issue<W, LPF, SPAN>(iq, mt, it0 + G * U, nr, grp, gl);
           sa.template consume<LPF>(ab, gl);
-          if ((it0 += G * U) >= total) { sb.template wait<0>(); break; }
-          sa.template issue<W, LPF, SPAN>(area, mt, it0 + G * U, total, grp, gl);
+          if ((it0 += G * U) >= nr) { sb.template wait<0>(); break; }
+          sa.template issue<W, LPF, SPAN>(iq, mt, it0 + G * U, nr, grp, gl);
           sb.template consume<LPF>(ab, gl);
-          if ((it0 += G * U) >= total) { sa.template wait<0>(); break; }
+          if ((it0 += G * U) >= nr) { sa.template wait<0>(); break; }
         }
       }
       // frames past the item budget: the whole wave sums each one
@@ -1033,9 +1045,9 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_split(const KernelArgs
       compiler_barrier();
       // ---- phase C: fold, check, store ----
       // an in-line check whose 64-byte sector lies in the frame and the window
-      // is written as that whole sector, patched in the window registers and
-      // staged in the (now free) slot area for the wave's coalesced store
-      LaneOut oc = {0, false, area + 64 * lane, r.fp};
+      // is written as that whole sector: patched in the lane's slot (the window
+      // is still there) and stored by the wave, as in phase A
+      LaneOut oc = {0, false, slot, r.fp};
       if (more) {
         const uint32_t s = part + args.payload_mult * lds_i32(ab + 4 * lane);   // :92-103
         const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));
@@ -1047,19 +1059,11 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_split(const KernelArgs
           res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
         } else if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
                    sec + 64 <= c0 + 16 * W) {
-          const int o = static_cast<int>(ck - c0);          // check offset in the window
-          const int j0 = static_cast<int>(sec - c0) >> 4;   // sector's first window chunk
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            uint4 x = v[0];
-#pragma unroll
-            for (int k = 1; k < W; ++k)
-              if (k == j0 + i) x = v[k];
-            x = put_byte(x, o - 16 * (j0 + i), c);
-            x = put_byte(x, o + 1 - 16 * (j0 + i), c >> 8);
-            lds_store_u128(oc.lds_sec + 16 * i, x);
-          }
+          const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
+          lds_store_u8(at, static_cast<uint8_t>(c));
+          lds_store_u8(at + 1, static_cast<uint8_t>(c >> 8));
           oc.sector = true;
+          oc.lds_sec = slot + static_cast<uint32_t>(sec - c0);
           oc.gsec = r.fp + static_cast<intptr_t>(sec - f0);
         } else {
           *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
@@ -1326,8 +1330,11 @@ __device__ __forceinline__ void scatter_sparse(const KernelArgs &args, uint8_t *
 
 __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) {
   __shared__ uint8_t which[kWavesPerBlock][kWave];     // record rank -> lane (sparse shape)
+  // The count only picks the shape: launches on other streams may share its
+  // counter set (more than kCountSlots / 2 in flight), so "no records" is never
+  // trusted to skip the pass -- the sparse scan (one 256-byte read and a ballot
+  // per 64 frames) finds any record.
   const uint32_t cnt = __builtin_amdgcn_readfirstlane(launch_records(args));
-  if (cnt == 0) return;                              // nothing parked (e.g. a mix written in-line)
   if (4ull * cnt >= args.n)
     scatter_dense(args);
   else
@@ -1445,8 +1452,9 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 4, 1, 0), XSKNF_S(5, 16, 2, 2, 0), XSKNF_S(4, 64, 2, 1, 0), XSKNF_S(4, 32, 2, 1, 0),
     XSKNF_S(7, 16, 2, 1, 0), XSKNF_S(4, 16, 3, 1, 0), XSKNF_S(4, 8, 2, 2, 0),
     XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
-    XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 16, 6, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
+    XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 32, 3, 1, 1),
+    XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
     XSKNF_L(5, 2),     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
