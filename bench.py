@@ -61,12 +61,21 @@ def parse():
 
 
 def dist_setup(args):
+    """One process per GPU (torch.distributed.run env).  XSKNF_BENCH_BACKEND=gloo
+    rehearses the N > 1 path on fewer GPUs (ranks share devices round robin);
+    the default is nccl (RCCL), one rank per GPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("XSKNF_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     if world != args.gpus:
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
@@ -79,16 +88,21 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
+def coll_device():
+    """Where collective operands live: HBM for RCCL, host memory for gloo."""
+    return "cuda" if os.environ.get("XSKNF_BENCH_BACKEND", "nccl") == "nccl" else "cpu"
+
+
 def allreduce_max(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def allreduce_sum_i64(vals, world):
-    t = torch.tensor(vals, dtype=torch.int64, device="cuda")
+    t = torch.tensor(vals, dtype=torch.int64, device=coll_device())
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [int(x) for x in t.tolist()]
