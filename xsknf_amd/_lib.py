@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libxsknf_gpu.so")
+# XSKNF_GPU_LIB: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("XSKNF_GPU_LIB") or os.path.join(_HERE, "lib", "libxsknf_gpu.so")
 
 # Every symbol include/xsknf_gpu.h declares (checked by tests/test_capi.py).
 EXPORTED_SYMBOLS = (
