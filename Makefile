@@ -16,8 +16,15 @@ APP := xsknf_amd/bin/checksummer
 
 all: $(LIB) $(RTLIB) $(APP) oracle
 
-$(LIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h Makefile
-	@mkdir -p $(LIBDIR)
+ASM := build/asm/checksummer-gfx950.s
+
+# The library is kept only if the device code passes tools/check_inflight.py:
+# no instruction may name a register of an inline-asm load before its counted
+# s_waitcnt (the compiler does not know those registers are still in flight).
+$(LIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h tools/check_inflight.py Makefile
+	@mkdir -p $(LIBDIR) build/asm
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o $(ASM) xsknf_amd/csrc/checksummer.hip
+	python3 tools/check_inflight.py $(ASM)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
 
 $(RTLIB): $(RTSRCS) $(RTHDRS) Makefile
@@ -40,7 +47,7 @@ $(VETH): tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c $(RTLIB) oracle
 # keep the device assembly for inspection (VGPRs, instruction mix)
 asm: $(SRCS)
 	@mkdir -p build/asm
-	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/asm/checksummer-gfx950.s xsknf_amd/csrc/checksummer.hip
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o $(ASM) xsknf_amd/csrc/checksummer.hip
 
 oracle:
 	$(MAKE) -C oracle

@@ -222,7 +222,8 @@ struct FrameRef {
 __device__ __forceinline__ FrameRef make_ref(const KernelArgs &a, uint64_t addr, uint32_t len, bool exists) {
   FrameRef r;
   const uint64_t off = umem_offset(addr);
-  const bool in_range = off <= a.umem_size && len <= a.umem_size - off;
+  // (frames of 2 GiB and more are treated as out of range: lengths are ints here)
+  const bool in_range = off <= a.umem_size && len <= a.umem_size - off && len < 0x80000000u;
   r.exists = exists;
   r.live = exists && in_range && len >= 14;
   r.len = static_cast<int>(len);
