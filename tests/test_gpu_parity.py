@@ -186,6 +186,8 @@ SHAPES = [
     (16, 2, 1, 0, 0, 1, 7), (16, 3, 1, 0, 2, 1, 4), (8, 2, 2, 0, 1, 1, 4),
     (16, 2, 2, 0, 0, 1, 20), (16, 3, 1, 0, 1, 1, 20), (16, 2, 1, 0, 5, 1, 20),
     (16, 3, 1, 0, 0, 1, 24), (16, 2, 2, 0, 1, 1, 24), (32, 3, 1, 0, 2, 1, 24), (16, 2, 1, 0, 1, 1, 24),
+    # + 16: deferred checks patched in the summing kernel's tail (no scatter launch)
+    (16, 3, 1, 0, 16, 1, 24), (16, 3, 1, 0, 18, 1, 24), (16, 2, 2, 0, 18, 1, 4), (16, 3, 2, 0, 20, 1, 20),
 ]
 
 
@@ -313,8 +315,9 @@ def test_huge_frames_take_the_whole_wave_path(dev, shape):
 def test_concurrent_streams(dev):
     """Many batches in flight at once on separate streams (as the AF_XDP hook
     runs one stream per worker): every one bit-exact.  The scatter pass's
-    per-launch record counters are shared by launches far enough apart, so
-    they may only steer its shape, never decide whether it runs."""
+    per-launch record counters (64 sets) are reused by launches 64 apart:
+    with more than 64 launches queued at once, a reused set must make the
+    pass scan, never skip (g_rec_count in checksummer.hip)."""
     nstreams = 24
     jobs = []
     for i in range(nstreams):
@@ -322,7 +325,7 @@ def test_concurrent_streams(dev):
         b = frames.aligned_batch(4096, length, chunk=2048, seed=100 + i)
         frames.inject_edge_cases(b, 0.05, seed=200 + i)
         ref = b.copy()
-        for _ in range(3):   # reprocessing is not idempotent for ihl 2/3 frames
+        for _ in range(4):   # reprocessing is not idempotent for ihl 2/3 frames
             ov = O.c_process_batch(ref.umem, ref.descs)
         jobs.append((b, ref.umem, ov, torch.cuda.Stream(device=dev)))
     outs = []
@@ -334,11 +337,11 @@ def test_concurrent_streams(dev):
     torch.cuda.synchronize()
     cs = Checksummer(frame_len_hint=1500)
     res = []
-    for rep in range(3):   # several launches per stream, none waited for in between
+    for rep in range(4):   # several launches per stream, none waited for in between
         for (umem, descs), (b, ou, ov, st) in zip(outs, jobs):
             with torch.cuda.stream(st):
                 res.append(cs.process_batch(umem, descs))
     torch.cuda.synchronize()
     for k, ((umem, descs), (b, ou, ov, st)) in enumerate(zip(outs, jobs)):
-        assert np.array_equal(res[2 * nstreams + k].cpu().numpy(), ov), f"stream {k}"
+        assert np.array_equal(res[3 * nstreams + k].cpu().numpy(), ov), f"stream {k}"
         assert np.array_equal(umem.cpu().numpy(), ou), f"stream {k}"

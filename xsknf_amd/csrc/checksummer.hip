@@ -340,7 +340,13 @@ __device__ __forceinline__ bool store_check_sector(const FrameRef &r, const Head
 // the step would cost ~60 VGPRs of occupancy for a rare case).
 constexpr uint32_t kPendTag = 0x80000000u;
 // kNoDefer (defer_min_len: every check in-line): checksummer_internal.h
-constexpr uint32_t kDeferMinLen = 1024;        // hybrid default (tools/tune.py: 64 B, 570 B
+#ifndef XSKNF_DEFER_MIN_LEN
+#define XSKNF_DEFER_MIN_LEN 1024
+#endif
+#ifndef XSKNF_DEFER_TILE_K   // a tile defers when K * (long frames) >= live frames
+#define XSKNF_DEFER_TILE_K 2
+#endif
+constexpr uint32_t kDeferMinLen = XSKNF_DEFER_MIN_LEN;        // hybrid default (tools/tune.py: 64 B, 570 B
                                                // and IMIX prefer in-line, 1500 B deferred)
 
 // Result word of a frame after its pass-0 sum P0 (group-reduced, last lane).
@@ -393,43 +399,57 @@ __device__ __forceinline__ void finish_long_frames(const KernelArgs &a, uint32_t
   }
 }
 
-// Records per launch, for the scatter pass to pick its shape (per device: a
-// __device__ variable exists once per GPU).  Launch `seq` adds to set
-// seq % kCountSlots and clears set (seq + kCountSlots / 2) % kCountSlots for a
-// later launch.  A set is 64 counters on
-// separate 64-byte lines (block b adds to counter b % 64): one shared address
-// would serialize every tile's atomic in one L2 channel.  Only speed depends on
-// the count: both scatter shapes are exact at any record density.
+// Records per launch, for the scatter pass to pick its shape and to skip
+// itself when nothing was parked (per device: a __device__ variable exists once
+// per GPU).  Launch `seq` publishes into set seq % kCountSlots, 64 counter words
+// on separate 64-byte lines (block b adds to word b % 64: one shared address
+// would serialize the publishing atomics in one L2 channel).  A word is
+// {launch seq (high 32 bits), records (low 32)}: a wave adds to it while it
+// carries its own seq and restarts it (CAS) while it carries an older one.  The
+// scatter pass sums the words tagged with its seq; words tagged older are a
+// zero of this launch; a word tagged NEWER means a launch kCountSlots later
+// reused the set while this one was in flight, and the count is unknown (the
+// pass then scans every frame).  So "no records" is exact when it is reported.
 constexpr uint32_t kCountSlots = 64;
 constexpr uint32_t kCountLanes = 64;
-constexpr uint32_t kCountStride = 16;          // u32 words = 64 bytes
-__device__ uint32_t g_rec_count[kCountSlots][kCountLanes][kCountStride];
+constexpr uint32_t kCountStride = 8;           // u64 words = 64 bytes
+constexpr uint32_t kCountUnknown = 0xffffffffu;
+__device__ unsigned long long g_rec_count[kCountSlots][kCountLanes][kCountStride];
 
 // Store a tile's result word (lane's frame); returns the tile's record count
 // (wave-uniform), which the wave adds up and publishes once, at exit: an
 // atomic per tile would hold every following vmcnt wait on its L2 round trip.
 __device__ __forceinline__ uint32_t store_result(const KernelArgs &a, uint32_t f, bool valid, int32_t v) {
   if (valid) a.verdicts[f] = v;
-  if (!a.count_records) return 0;
+  if (!a.count_records && !a.tail_scatter) return 0;
   return static_cast<uint32_t>(__builtin_popcountll(
       __builtin_amdgcn_ballot_w64(valid && (static_cast<uint32_t>(v) & kRecTagMask) == kRecTag)));
 }
 
 __device__ __forceinline__ void publish_records(const KernelArgs &a, uint32_t nrec, int lane) {
-  if (a.count_records && lane == 0 && nrec)
-    atomicAdd(&g_rec_count[a.seq % kCountSlots][blockIdx.x % kCountLanes][0], nrec);
+  if (!a.count_records || lane != 0 || !nrec) return;
+  unsigned long long *w = &g_rec_count[a.seq % kCountSlots][blockIdx.x % kCountLanes][0];
+  unsigned long long old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    const uint32_t tag = static_cast<uint32_t>(old >> 32);
+    if (tag == a.seq) { atomicAdd(w, static_cast<unsigned long long>(nrec)); return; }
+    if (static_cast<int32_t>(tag - a.seq) > 0) return;   // a newer launch owns the word
+    const unsigned long long mine = (static_cast<unsigned long long>(a.seq) << 32) | nrec;
+    const unsigned long long prev = atomicCAS(w, old, mine);
+    if (prev == old) return;
+    old = prev;
+  }
 }
 
-__device__ __forceinline__ void clear_next_count(const KernelArgs &a) {
-  if (a.count_records && blockIdx.x == 0 && threadIdx.x < kCountLanes)
-    g_rec_count[(a.seq + kCountSlots / 2) % kCountSlots][threadIdx.x][0] = 0;
-}
-
-// The launch's record count, on every lane (wave-wide sum of the 64 counters).
+// The launch's record count on every lane (kCountUnknown if the set was reused).
 __device__ __forceinline__ uint32_t launch_records(const KernelArgs &a) {
   const int lane = threadIdx.x & (kWave - 1);
-  uint32_t c = __hip_atomic_load(&g_rec_count[a.seq % kCountSlots][lane % kCountLanes][0], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long w = __hip_atomic_load(&g_rec_count[a.seq % kCountSlots][lane % kCountLanes][0],
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t tag = static_cast<uint32_t>(w >> 32);
+  uint32_t c = tag == a.seq ? static_cast<uint32_t>(w) : 0u;
+  const bool newer = tag != a.seq && static_cast<int32_t>(tag - a.seq) > 0;
+  if (__builtin_amdgcn_ballot_w64(newer)) return kCountUnknown;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) c += static_cast<uint32_t>(__shfl_xor(static_cast<int>(c), o, kWave));
   return c;
@@ -514,7 +534,6 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
   const uint32_t dsc = lds_addr(&dtile[wv][0]);
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t last = args.n - 1;
-  clear_next_count(args);
 
   // the next tile's descriptors ride in VGPRs (lane l: frame l of the tile)
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
@@ -533,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(lane < T && tf0 + lane < args.n && dnext.z >= args.defer_min_len)));
       const uint32_t nlive = min(static_cast<uint32_t>(T), args.n - tf0);
-      if (2 * nlong < nlive) ta.defer_min_len = kNoDefer;
+      if (XSKNF_DEFER_TILE_K * nlong < nlive) ta.defer_min_len = kNoDefer;
     }
     dnext = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * T + min(lane, T - 1), last));
 
@@ -687,7 +706,6 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs 
   const uint32_t slot = lds_addr(&hdr[wv][lane][0]);
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t last = args.n - 1;
-  clear_next_count(args);
 
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
   uint32_t nrec = 0;
@@ -869,6 +887,62 @@ struct ItemStage {
   }
 };
 
+// The deferred checks of a wave's own tiles, patched by the wave itself after
+// its last tile (KernelArgs::tail_scatter): the write-only pass of
+// scatter_checks without a second launch, and without waiting for the slowest
+// wave of the grid.  The wave's record stores are complete (vmcnt 0) before it
+// reads them back (non-temporal loads: from L2, where they landed).  A tile
+// with no record costs one 256-byte read.  Per round 16 frames, 4 lanes each,
+// as the dense scatter shape: the lanes of a frame rewrite its check's 64-byte
+// sector with one non-temporal store (2 bytes where the sector leaves the frame).
+__device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t tile0, uint32_t waves, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int piece = lane & 3;
+  for (uint32_t tile = tile0; tile * kWave < args.n; tile += waves) {
+    const uint32_t f = tile * kWave + lane;
+    const uint32_t r = f < args.n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(args.verdicts) + f)
+                                  : 0u;
+    const bool rec = (r & kRecTagMask) == kRecTag;
+    if (!__builtin_amdgcn_ballot_w64(rec)) continue;
+    uint32_t rr[4];
+    xsknf_gpu_desc d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int src = 16 * k + (lane >> 2);
+      rr[k] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(r)));
+      d[k] = args.descs[min(tile * kWave + src, args.n - 1)];
+    }
+    uint4 v[4];
+    uint8_t *mine[4];
+    int o[4];
+    bool whole[4], has[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      has[k] = (rr[k] & kRecTagMask) == kRecTag;   // src < n: records exist only there
+      uint8_t *fp = args.umem + umem_offset(d[k].addr);
+      uint8_t *chk = fp + ((rr[k] >> 16) & 0x7f) + 6;
+      uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);   // keeps global addressing
+      whole[k] = has[k] && sec >= fp && sec + 64 <= fp + d[k].len && (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
+      mine[k] = whole[k] ? sec + 16 * piece : chk;
+      o[k] = static_cast<int>(chk - mine[k]);
+      if (whole[k]) v[k] = load_nt(reinterpret_cast<const uint4 *>(mine[k]));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint16_t c = static_cast<uint16_t>(rr[k]);
+      if (whole[k]) {
+        uint4 w = put_byte(v[k], o[k], c);
+        w = put_byte(w, o[k] + 1, c >> 8);
+        store_nt16(mine[k], w);
+      } else if (has[k] && piece == 0) {
+        mine[k][0] = static_cast<uint8_t>(c);
+        mine[k][1] = static_cast<uint8_t>(c >> 8);
+      }
+    }
+    if (rec) args.verdicts[f] = args.fwd_verdict;
+  }
+}
+
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
 // +8-11 % from 2 -> 3 waves per SIMD, so the register budget is pinned.
@@ -899,7 +973,6 @@ void checksum_kernel_split(const KernelArgs args) {
   const uint32_t iq = lds_addr(&itemq[wv][0]);
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t last = args.n - 1;
-  clear_next_count(args);
 
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
   uint32_t nrec = 0;
@@ -944,7 +1017,7 @@ void checksum_kernel_split(const KernelArgs args) {
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(f < args.n && d.z >= defer_min)));
       const uint32_t nlive = min(static_cast<uint32_t>(kWave), args.n - tile * kWave);
-      if (2 * nlong < nlive) defer_min = kNoDefer;
+      if (XSKNF_DEFER_TILE_K * nlong < nlive) defer_min = kNoDefer;
     }
 
     // ---- phase A: header, window sum, short frames finished ----
@@ -1078,7 +1151,12 @@ void checksum_kernel_split(const KernelArgs args) {
     d = dn;
     dn = dnn;
   }
-  publish_records(args, nrec, lane);
+  if (args.tail_scatter) {
+    if (__builtin_amdgcn_readfirstlane(nrec))
+      tail_scatter(args, blockIdx.x * kWavesPerBlock + wv, waves, lane);
+  } else {
+    publish_records(args, nrec, lane);
+  }
 }
 
 // ---- LDS-DMA ring kernel ------------------------------------------------------
@@ -1134,7 +1212,6 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   const uint32_t wg = blockIdx.x * kWavesPerBlock + wv;
   const uint32_t last = args.n - 1;
-  clear_next_count(args);
 
   // Step j of this wave covers tile k = j / SPT (global tile wg + k*waves),
   // frames (j % SPT)*G + grp of it.  Tile k's descriptors sit in dtile[k & 1],
@@ -1331,12 +1408,12 @@ __device__ __forceinline__ void scatter_sparse(const KernelArgs &args, uint8_t *
 
 __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) {
   __shared__ uint8_t which[kWavesPerBlock][kWave];     // record rank -> lane (sparse shape)
-  // The count only picks the shape: launches on other streams may share its
-  // counter set (more than kCountSlots / 2 in flight), so "no records" is never
-  // trusted to skip the pass -- the sparse scan (one 256-byte read and a ballot
-  // per 64 frames) finds any record.
+  // nothing parked: done (exact, see g_rec_count); an unknown count (the
+  // counter set was reused by a later launch in flight) takes the sparse scan,
+  // which finds any record
   const uint32_t cnt = __builtin_amdgcn_readfirstlane(launch_records(args));
-  if (4ull * cnt >= args.n)
+  if (cnt == 0) return;
+  if (cnt != kCountUnknown && 4ull * cnt >= args.n)
     scatter_dense(args);
   else
     scatter_sparse(args, which[threadIdx.x / kWave]);
@@ -1395,7 +1472,7 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
 
 int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess && a.defer_min_len != kNoDefer && !a.no_scatter) {
+  if (e == hipSuccess && a.defer_min_len != kNoDefer && !a.no_scatter && !a.tail_scatter) {
     const uint32_t need = (4 * a.n + kBlock - 1) / kBlock;   // dense shape: 4 lanes per frame
     const uint32_t cap = static_cast<uint32_t>(device_cus() * 8);
     hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
@@ -1535,6 +1612,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
   a.no_scatter = 0;
   a.sector_stores = 1;
   a.plain_sector = 0;
+  a.tail_scatter = 0;
   a.seq = 0;
   a.count_records = 0;
   // aligned-down descriptor address: inside the descriptor array's own page
@@ -1545,7 +1623,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
   const int mode = cfg.fused_stores & 3;          // + 4: 2-byte in-line stores, + 8: plain sector stores
-  if (cfg.fused_stores < 0 || cfg.fused_stores > 15) return -EINVAL;
+  if (cfg.fused_stores < 0 || cfg.fused_stores > 31) return -EINVAL;
   const Variant *v = find_variant(cfg);
   if (!v) return -EINVAL;
   KernelArgs a = base;
@@ -1553,9 +1631,12 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (mode == 3) a.no_scatter = 1;   // records only: the caller applies the checks
   if (cfg.fused_stores & 4) a.sector_stores = 0;
   if (cfg.fused_stores & 8) a.plain_sector = 1;
+  // + 16: the split kernel patches its deferred checks itself (no scatter launch)
+  a.tail_scatter = (cfg.fused_stores & 16) && v->kernel == XSKNF_GPU_KERNEL_SPLIT && a.defer_min_len != kNoDefer &&
+                   !a.no_scatter;
   static std::atomic<uint32_t> seq{0};
   a.seq = seq.fetch_add(1, std::memory_order_relaxed);
-  a.count_records = a.defer_min_len != kNoDefer && !a.no_scatter;
+  a.count_records = a.defer_min_len != kNoDefer && !a.no_scatter && !a.tail_scatter;
   return v->fn(a, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
 }
 

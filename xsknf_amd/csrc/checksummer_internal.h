@@ -29,6 +29,8 @@ struct KernelArgs {
                            // no read-modify-write); 0: 2-byte stores (host memory)
   uint32_t plain_sector;   // 1: whole-sector stores of the lane kernel are plain (write-back),
                            // 0: non-temporal
+  uint32_t tail_scatter;   // 1 (split kernel): each wave patches the deferred checks of its
+                           // own tiles after its last tile; no scatter launch
 };
 
 // Check record parked in verdicts[f] by the summing pass (deferred stores):
