@@ -1571,7 +1571,8 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   // the split kernel with the transposed (coalesced) header-window load for
   // every size class (group kernels in brackets).
   //  * hint <= 128: 4-chunk window, 16 x 2 items, every check in-line (short
-  //    frames as whole 64-byte sectors), no scatter launch: 64 B 40 us [50];
+  //    frames as whole 64-byte sectors, plain write-back stores: 64 B 38.1 us,
+  //    non-temporal 38.7; 570 B 142 vs 147), no scatter launch: 64 B 40 us [50];
   //  * < 1 KiB: 8-chunk window (the frame's whole first 128-byte line, so
   //    phase B never refetches it): 570 B 144 us [175];
   //  * < 4 KiB: 8-chunk window, 16 x 3 items, the per-tile policy defers the
@@ -1582,9 +1583,9 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.kernel = XSKNF_GPU_KERNEL_SPLIT;
   c.lanes_per_frame = 16;
   if (hint <= 128) {
-    c.window_chunks = 4 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1;
+    c.window_chunks = 4 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1 + 8;
   } else if (hint < kDeferMinLen) {
-    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1;
+    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1 + 8;
   } else if (hint + 15 <= 4096) {
     c.window_chunks = 8 + 16; c.chunks_per_lane = 3; c.frames_per_group = 1; c.fused_stores = 0;
   } else {
