@@ -128,6 +128,33 @@ def test_out_of_range_descriptors_are_dropped_untouched(dev):
     assert np.array_equal(gu, ou)
 
 
+@pytest.mark.parametrize("hint", [0, 64, 1500, 9000])
+def test_frames_ending_at_the_umem_end(dev, hint):
+    """A UMEM whose size is not a multiple of 16 and whose last frames end on
+    its last byte (odd starts): the 16-byte chunk loads may not change any
+    result there; a frame one byte too long is dropped untouched."""
+    rng = np.random.default_rng(hint + 5)
+    lens = rng.integers(14, 2000, size=300).astype(np.uint32)
+    lens[-4:] = (60, 7, 33, 1501)
+    b = frames.unaligned_batch(300, lens, seed=hint + 5)
+    frames.inject_edge_cases(b, 0.05, seed=hint + 6)
+    addr = b.descs["addr"]
+    offs = (addr & np.uint64((1 << 48) - 1)) + (addr >> np.uint64(48))
+    end = int((offs + b.descs["len"]).max())
+    last = int(np.argmax(offs + b.descs["len"]))
+    t = frames.HostBatch(b.umem[:end].copy(), b.descs.copy(), "unaligned")
+    assert_parity(t, dev, hint=hint, iters=2)
+    over = frames.HostBatch(b.umem[:end].copy(), b.descs.copy(), "unaligned")
+    over.descs["len"][last] += 1                     # one byte past the UMEM
+    gu, gv = run_gpu(over, dev, hint=hint)
+    assert gv[last] == -1
+    keep = np.ones(over.n, bool)
+    keep[last] = False
+    ou, ov = run_oracle(frames.HostBatch(over.umem.copy(), over.descs[keep].copy(), "unaligned"))
+    assert np.array_equal(gv[keep], ov)
+    assert np.array_equal(gu, ou)
+
+
 def test_reprocessing(dev):
     """A second pass over processed frames matches the oracle run on them, and on
     well-formed frames (ihl 5) it changes nothing: the check is cleared before
