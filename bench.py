@@ -57,6 +57,9 @@ def parse():
                    help="threads for the all-cores CPU leg (-1 = the process's CPUs, at most 16; 0 = skip)")
     p.add_argument("--min-warmup-s", type=float, default=0.1,
                    help="keep warming up (untimed) until this much time has passed")
+    p.add_argument("--root-scatter", action="store_true",
+                   help="N > 1: also time the distribution of a root-resident global IMIX batch "
+                        "(SURVEY 8(e) collective 1), reported as `root_scatter`")
     p.add_argument("--kernel-steps", type=int, default=50,
                    help="launches of the summing kernel alone for the roofline (0 = skip)")
     return p.parse_args()
@@ -206,6 +209,63 @@ def time_workload(name, args, world, rank, dev, seed):
     return res
 
 
+def root_scatter_leg(args, world, rank, dev):
+    """SURVEY.md 8(e), collective 1 (and BASELINE config 4's shape): the global
+    batch -- `--frames` x world IMIX frames, packed (unaligned-mode) -- starts in
+    rank 0's HBM; each rank receives its byte-balanced contiguous shard (one
+    span + its descriptors, point-to-point over xGMI, all ranks at once) and
+    checksums it.  Reported separately from `value`: the device-resident metric
+    excludes the distribution, and in the reference frames arrive per NIC queue."""
+    from xsknf_amd.shard import scatter_from_root, shard_by_bytes
+    n_total = args.frames * world
+    umem = descs = ranges = None
+    if rank == 0:
+        umem, dt, lens = frames.device_batch(n_total, "imix", layout="unaligned", seed=frames.SEED, device=dev)
+        descs = dt.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1)
+        ranges = shard_by_bytes(lens, world)
+        del dt
+    cdev = coll_device()
+    if cdev == "cpu" and umem is not None:     # gloo rehearsal: host tensors
+        umem = umem.cpu()
+    barrier(world)
+    t0 = time.perf_counter()
+    lu, ld, (b0, b1) = scatter_from_root(dist, umem, descs, ranges, rank, world, cdev)
+    if cdev == "cuda":
+        torch.cuda.synchronize()
+    barrier(world)
+    t_move = allreduce_max(time.perf_counter() - t0, world)
+    if cdev == "cpu":
+        lu, ld = lu.to(dev), ld.to(dev)
+    n_local = ld.shape[0]
+    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=1500)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(3):
+        v = cs.process_batch(lu, ld)
+    barrier(world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    reps = 10
+    for _ in range(reps):
+        v = cs.process_batch(lu, ld)
+    e1.record(stream)
+    barrier(world)
+    step_s = allreduce_max(e0.elapsed_time(e1) / reps / 1e3, world)
+    dl = ld.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1)
+    vh = v.cpu().numpy()
+    moved = (b1 - b0 + 16 * n_local) if rank != 0 else 0
+    tot = allreduce_sum_i64([n_local, int(dl["len"].astype(np.int64).sum()), moved,
+                             int((vh == -1).sum()), int((vh >= 0).sum())], world)
+    if rank == 0 and tot[0] != n_total:
+        raise RuntimeError(f"root scatter: {tot[0]} frames arrived of {n_total}")
+    return {"frames_total": tot[0], "frame_bytes_total": tot[1], "bytes_moved": tot[2],
+            "scatter_ms": round(t_move * 1e3, 3),
+            "scatter_GBps": round(tot[2] / t_move / 1e9, 1) if t_move > 0 else None,
+            "checksum_step_us_max": round(step_s * 1e6, 2),
+            "gbs_checksummed": round(tot[1] / step_s / 1e9, 1),
+            "verdicts": {"drop": tot[3], "forward": tot[4]},
+            "layout": "IMIX 64/570/1500 (7:4:1) packed, unaligned-mode descriptors; shards by bytes"}
+
+
 def cpu_baseline(res, budget_s, threads, check=True):
     """Oracle (the C restatement, gcc -O2 -flto) timed on host cores over a bounded
     sample of the same workload; also checks the GPU result on that sample."""
@@ -264,6 +324,8 @@ def main():
                      "sum_kernel_us": round(r["sum_ms"] * 1e3, 2) if r["sum_ms"] else None}
         del r
 
+    root_scatter = root_scatter_leg(args, world, rank, dev) if (args.root_scatter and world > 1) else None
+
     total_frames, total_bytes, n_drop, n_fwd = prim["counters"]
     step_s = prim["wall_max"] / args.steps
     value = total_bytes / step_s / 1e9
@@ -312,6 +374,8 @@ def main():
             "roofline": roof, "cpu_baseline": cpu, "secondary": sec,
             "verdicts": {"drop": n_drop, "forward": n_fwd},
         }
+        if root_scatter is not None:
+            out["root_scatter"] = root_scatter
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

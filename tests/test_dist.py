@@ -61,3 +61,44 @@ def test_two_rank_gloo_shards_and_counters():
     assert total == out[1][2]
     assert total[0] == b.n and total[1] == int(b.descs["len"].astype(np.int64).sum())
     assert total[2] + total[3] == b.n
+
+
+def _root_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import csum_oracle as O
+    from xsknf_amd.shard import scatter_from_root
+    umem = descs = ranges = None
+    if rank == 0:
+        b = frames.unaligned_batch(3000, "imix", seed=21)
+        frames.inject_edge_cases(b, 0.05, seed=22)
+        umem, descs = torch.from_numpy(b.umem.copy()), b.descs
+        ranges = shard_by_bytes(b.descs["len"], world)
+    lu, ld, (b0, b1) = scatter_from_root(dist, umem, descs, ranges, rank, world, "cpu")
+    u = lu.numpy().copy()
+    d = ld.numpy().view(frames.DESC_DTYPE).reshape(-1).copy()
+    v = O.c_process_batch(u, d)
+    out[rank] = (b0, b1, u[:b1 - b0].tobytes(), v.tolist())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_root_scatter_shards_are_bit_exact(world):
+    """bench.py --root-scatter's distribution (collective 1) on
+    gloo: every rank checksums the shard it received, and the bytes and
+    verdicts equal the oracle's pass over the whole batch on the root."""
+    from oracle import csum_oracle as O
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_root_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    b = frames.unaligned_batch(3000, "imix", seed=21)
+    frames.inject_edge_cases(b, 0.05, seed=22)
+    ranges = shard_by_bytes(b.descs["len"], world)
+    full = b.umem.copy()
+    fv = O.c_process_batch(full, b.descs)
+    for r in range(world):
+        b0, b1, ub, v = out[r]
+        lo, hi = ranges[r]
+        assert v == fv[lo:hi].tolist(), f"rank {r} verdicts"
+        assert ub == full[b0:b1].tobytes(), f"rank {r} bytes"

@@ -43,3 +43,94 @@ def allreduce_counters(dist, local: np.ndarray, device="cpu") -> np.ndarray:
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.cpu().numpy()
+
+
+# ---- root distribution (collective 1) ------------------------
+#
+# When a global batch originates on one GPU (rank 0), the other ranks get
+# their shards over xGMI before checksumming: each rank's frames occupy one
+# contiguous byte span of the root's UMEM (contiguous descriptor ranges of a
+# packed rx layout), so a shard moves as ONE point-to-point transfer of that
+# span plus its descriptors, all ranks at once (batch_isend_irecv: the root's
+# links run in parallel), not a ring collective.  This is not on the hot path
+# (frames arrive per NIC queue, i.e. per worker, in the reference) and is
+# measured separately (bench.py --root-scatter).
+
+def effective_offsets(descs) -> np.ndarray:
+    """UMEM byte offset of every frame (aligned or unaligned-mode addresses, as
+    xsk_umem__add_offset_to_addr() translates them, src/xsknf.c:659)."""
+    a = np.asarray(descs["addr"], dtype=np.uint64)
+    return ((a & np.uint64((1 << 48) - 1)) + (a >> np.uint64(48))).astype(np.int64)
+
+
+def _in_umem(descs, umem_size: int) -> np.ndarray:
+    offs = effective_offsets(descs)
+    return (offs <= umem_size) & (np.asarray(descs["len"], dtype=np.int64) <= umem_size - offs)
+
+
+def shard_spans(descs, ranges, umem_size: int) -> list:
+    """(b0, b1): the byte span of the UMEM holding each rank's frames
+    (descriptors outside the UMEM hold no bytes)."""
+    offs = effective_offsets(descs)
+    ends = offs + np.asarray(descs["len"], dtype=np.int64)
+    ok = _in_umem(descs, umem_size)
+    out = []
+    for lo, hi in ranges:
+        m = ok[lo:hi]
+        out.append((int(offs[lo:hi][m].min()), int(ends[lo:hi][m].max())) if m.any() else (0, 0))
+    return out
+
+
+OUT_OF_RANGE = np.uint64(1 << 47)   # an address past any UMEM: the frame is dropped untouched
+
+
+def rebase_descs(descs, b0: int, umem_size: int) -> np.ndarray:
+    """The same frames as plain (offset-free) addresses relative to byte b0;
+    a descriptor outside the UMEM stays outside it (verdict -1, no bytes)."""
+    from .frames import DESC_DTYPE
+    out = np.zeros(len(descs), dtype=DESC_DTYPE)
+    rel = (effective_offsets(descs) - b0).astype(np.uint64)
+    out["addr"] = np.where(_in_umem(descs, umem_size), rel, OUT_OF_RANGE)
+    out["len"] = descs["len"]
+    out["options"] = descs["options"]
+    return out
+
+
+def scatter_from_root(dist, umem, descs, ranges, rank: int, world: int, device, root: int = 0):
+    """Move every rank's shard from the root.  On the root: `umem` is the whole
+    UMEM (uint8 tensor on `device`), `descs` the whole descriptor array
+    (frames.DESC_DTYPE, host), `ranges` from shard_by_bytes(); elsewhere they
+    are ignored.  Returns (local umem tensor, local descs as an (n, 2) int64
+    tensor of xdp_desc bytes, (b0, b1)).  The root's own shard is a view."""
+    import torch
+    meta = torch.zeros((world, 3), dtype=torch.int64, device=device)
+    spans = None
+    if rank == root:
+        spans = shard_spans(descs, ranges, umem.numel())
+        meta.copy_(torch.tensor([[b0, b1, hi - lo] for (b0, b1), (lo, hi) in zip(spans, ranges)],
+                                dtype=torch.int64))
+    dist.broadcast(meta, src=root)
+    b0, b1, n = (int(x) for x in meta[rank].tolist())
+    ops = []
+    if rank == root:
+        for r in range(world):
+            lo, hi = ranges[r]
+            rb0, rb1 = spans[r]
+            d = rebase_descs(descs[lo:hi], rb0, umem.numel())
+            d = torch.from_numpy(d.view(np.int64).reshape(-1, 2).copy()).to(device)
+            if r == root:
+                local = (umem[rb0:rb1], d)
+            else:
+                ops.append(dist.P2POp(dist.isend, umem[rb0:rb1].contiguous(), r))
+                ops.append(dist.P2POp(dist.isend, d, r))
+    else:
+        # 16 spare bytes: the kernel's 16-byte chunk loads may end past the span
+        buf = torch.empty(b1 - b0 + 16, dtype=torch.uint8, device=device)
+        d = torch.empty((n, 2), dtype=torch.int64, device=device)
+        ops.append(dist.P2POp(dist.irecv, buf[:b1 - b0], root))
+        ops.append(dist.P2POp(dist.irecv, d, root))
+        local = (buf, d)
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return local[0], local[1], (b0, b1)
