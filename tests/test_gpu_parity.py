@@ -302,9 +302,13 @@ def test_host_path_bit_exact(dev, path, layout):
     cs = Checksummer(ChecksummerOptions(action=O.REDIRECT, csum_iterations=3), num_interfaces=2,
                      frame_len_hint=1500)
     umem = b.umem.copy()
+    # batch sizes across the zero-copy shapes: split kernel (> 2048 frames),
+    # group kernels 32 x 3 (<= 256) and 64 x 2 (<= 2048)
+    cuts = np.cumsum([0, 2100, 64, 200, 636])
+    assert cuts[-1] == b.n
     with HostPath(cs, umem, path=path, max_batch=4096) as hp:
-        v = np.concatenate([hp.process_batch(b.descs[i:i + 700], ingress_ifindex=1)
-                            for i in range(0, b.n, 700)])
+        v = np.concatenate([hp.process_batch(b.descs[lo:hi], ingress_ifindex=1)
+                            for lo, hi in zip(cuts[:-1], cuts[1:])])
         st = hp.stats()
     assert st["frames"] == b.n
     assert np.array_equal(v, ov)

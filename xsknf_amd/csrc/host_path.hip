@@ -41,8 +41,22 @@ struct xsknf_gpu_ctx {
   int32_t *verdicts_dev = nullptr;
   xsknf_gpu_desc *descs_pinned = nullptr;
   int32_t *verdicts_pinned = nullptr;
+  xsknf_gpu_desc *descs_mapped = nullptr;   // device views of the pinned arrays (direct mode)
+  int32_t *verdicts_mapped = nullptr;
   xsknf_gpu_ctx_stats stats = {};
 };
+
+// Direct mode (the default): the kernel reads the descriptors from, and
+// writes the verdicts / records to, the pinned host arrays themselves, so a
+// call is one launch and one synchronize -- no H2D descriptor copy and no D2H
+// verdict copy, each a separate DMA command with its own latency (a batch of 64
+// frames: 39 us per call with both copies).  -DXSKNF_CTX_COPY_ARRAYS keeps the
+// copies (A/B builds).
+#ifdef XSKNF_CTX_COPY_ARRAYS
+constexpr bool kDirect = false;
+#else
+constexpr bool kDirect = true;
+#endif
 
 namespace {
 
@@ -90,6 +104,8 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
   if (e == hipSuccess) e = hipMalloc(&c->verdicts_dev, sizeof(int32_t) * max_batch);
   if (e == hipSuccess) e = hipHostMalloc(&c->descs_pinned, sizeof(xsknf_gpu_desc) * max_batch, hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc(&c->verdicts_pinned, sizeof(int32_t) * max_batch, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->descs_mapped), c->descs_pinned, 0);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->verdicts_mapped), c->verdicts_pinned, 0);
   if (e != hipSuccess) {
     const int rc = fail(e, "xsknf_gpu_ctx_create");
     release(c);
@@ -132,19 +148,35 @@ int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *c, const struct xsknf_gpu_
   if (n == 0) return 0;
   if (!descs || !verdicts) return -EINVAL;
   KernelArgs a;
-  int rc = prepare(a, c->umem_dev, c->umem_size, c->descs_dev, n, ingress_ifindex, opts, c->verdicts_dev);
+  int rc = prepare(a, c->umem_dev, c->umem_size, kDirect ? c->descs_mapped : c->descs_dev, n, ingress_ifindex,
+                   opts, kDirect ? c->verdicts_mapped : c->verdicts_dev);
   if (rc != 0) return rc < 0 ? rc : 0;
   hipError_t e = hipSetDevice(c->device);
   if (e != hipSuccess) return fail(e, "hipSetDevice");
 
   memcpy(c->descs_pinned, descs, sizeof(xsknf_gpu_desc) * n);
-  e = hipMemcpyAsync(c->descs_dev, c->descs_pinned, sizeof(xsknf_gpu_desc) * n, hipMemcpyHostToDevice,
-                     c->stream);
-  if (e != hipSuccess) return fail(e, "hipMemcpyAsync(descs)");
+  if (!kDirect) {
+    e = hipMemcpyAsync(c->descs_dev, c->descs_pinned, sizeof(xsknf_gpu_desc) * n, hipMemcpyHostToDevice,
+                       c->stream);
+    if (e != hipSuccess) return fail(e, "hipMemcpyAsync(descs)");
+  }
   c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
 
   xsknf_gpu_launch_cfg cfg;
   default_cfg(c->hint ? c->hint : 2048u, cfg);
+  if (c->path == XSKNF_GPU_PATH_ZEROCOPY && n <= 2048) {
+    // A small batch is a few 64-frame tiles: the split kernel would read it
+    // over PCIe with a few waves.  The group kernel spreads it over many
+    // (4 or 2 frames per wave), so more reads are in flight
+    // (tools/small_batch.py, 1500 B: 64 frames 44.8 -> 18.8 us per call,
+    // 256: 46.8 -> 24.1, 1024: 51.0 -> 45.0; equal from 4096).
+    cfg.kernel = XSKNF_GPU_KERNEL_AUTO;
+    cfg.window_chunks = 0;
+    cfg.lds_ring = 0;
+    cfg.lanes_per_frame = n <= 256 ? 32 : 64;
+    cfg.chunks_per_lane = n <= 256 ? 3 : 2;
+    cfg.frames_per_group = n <= 256 ? 2 : 4;
+  }
   if (c->path == XSKNF_GPU_PATH_STAGED) {
     // byte span of the batch's (in-range) frames
     uint64_t lo = UINT64_MAX, hi = 0;
@@ -166,7 +198,9 @@ int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *c, const struct xsknf_gpu_
   }
   rc = run(a, cfg, c->stream);
   if (rc != 0) return rc;
-  e = hipMemcpyAsync(c->verdicts_pinned, c->verdicts_dev, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream);
+  e = kDirect ? hipSuccess
+              : hipMemcpyAsync(c->verdicts_pinned, c->verdicts_dev, sizeof(int32_t) * n, hipMemcpyDeviceToHost,
+                               c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) return fail(e, "verdict copy-back");
   c->stats.bytes_d2h += sizeof(int32_t) * n;
