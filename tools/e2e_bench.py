@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--batches", default="64,1024,16384,262144,1048576")
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--paths", default="zerocopy,staged")
     a = ap.parse_args()
     b = frames.aligned_batch(a.frames, a.len)
     ref = None
@@ -38,7 +39,7 @@ def main():
         O.c_process_batch(ref.umem, ref.descs)
     cs = Checksummer(frame_len_hint=a.len)
     results = []
-    for path in ("zerocopy", "staged"):
+    for path in a.paths.split(","):
         umem = b.umem.copy()
         with HostPath(cs, umem, path=path, max_batch=max(int(x) for x in a.batches.split(","))) as hp:
             for bs in [int(x) for x in a.batches.split(",")]:

@@ -36,6 +36,16 @@ def main():
     descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).pin_memory()
     verd = torch.empty(nmax, dtype=torch.int32).pin_memory()
     opts = _lib.CsumOpts(1, 0, 1, 0)
+    # floor: an (almost) empty launch + synchronize on the same device
+    x = torch.zeros(1, device="cuda")
+    ts = []
+    for i in range(a.calls + 20):
+        t0 = time.perf_counter()
+        x.add_(1)
+        torch.cuda.synchronize()
+        if i >= 20:
+            ts.append(time.perf_counter() - t0)
+    print(json.dumps({"null_launch_sync_us": round(statistics.median(ts) * 1e6, 2)}), flush=True)
     for n in (int(x) for x in a.batches.split(",")):
         for t in a.shapes.split(":"):
             s = tuple(int(y) for y in t.split(",")) + (0, 0)
