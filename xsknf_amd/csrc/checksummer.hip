@@ -826,7 +826,7 @@ __device__ __forceinline__ Payload payload_of(uint4 m) {
 // s_waitcnt), so no use can move above the wait, and a stage that is never
 // consumed is drained before its registers can be reused.
 __device__ __forceinline__ u32x4 gload_nt_asm(gchunk_ptr p) {
-  u32x4 x;
+  u32x4 x;   // nt: default-policy loads measured 1500 B 296 -> 344 us per step
   asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(x) : "v"(p) : "memory");
   return x;
 }
@@ -997,7 +997,7 @@ void checksum_kernel_split(const KernelArgs args) {
         const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
         const int nc = __builtin_amdgcn_ds_bpermute(g << 2, r.nch);
         const gchunk_ptr cp = reinterpret_cast<gchunk_ptr>((static_cast<uintptr_t>(hi) << 32) | lo);
-        x[p] = cp[min(lane % W, nc - 1)];
+        x[p] = cp[min(lane % W, nc - 1)];   // default policy: nt measured 64 B 39 -> 55 us, 1500 B 292 -> 308
       }
       compiler_barrier();
 #pragma unroll
@@ -1357,7 +1357,7 @@ __device__ __forceinline__ void scatter_dense(const KernelArgs &args) {
       whole[k] = rec[k] && sec >= fp && sec + 64 <= fp + d[k].len && (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
       mine[k] = whole[k] ? sec + 16 * (t & 3) : chk;
       o[k] = static_cast<int>(chk - mine[k]);
-      if (whole[k]) v[k] = load_nt(reinterpret_cast<const uint4 *>(mine[k]));
+      if (whole[k]) v[k] = load_nt(reinterpret_cast<const uint4 *>(mine[k]));   // plain: 296 -> 311 us
     }
 #pragma unroll
     for (int k = 0; k < kScatterU; ++k) {
