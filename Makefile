@@ -37,7 +37,15 @@ $(APP): xsknf_amd/csrc/checksummer_app.c $(RTLIB) $(LIB) include/xsknf.h include
 
 # config-1 harness (test / measurement infra: links the CPU oracle as the NF)
 VETH := tools/build/xsk_veth
-tools: $(VETH)
+PROBE := tools/build/hbm_probe
+PROBELIB := tools/build/libhbm_probe.so
+tools: $(VETH) $(PROBE) $(PROBELIB)
+$(PROBE): tools/hbm_probe.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Wno-inline-asm -o $@ $<
+$(PROBELIB): tools/hbm_probe.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) -O3 -std=c++17 -fPIC -shared -fvisibility=hidden -DHBM_PROBE_LIB --offload-arch=$(ARCH) -Wno-inline-asm -o $@ $<
 $(VETH): tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c $(RTLIB) oracle
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c \

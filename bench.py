@@ -295,6 +295,49 @@ def cpu_baseline(res, budget_s, threads, check=True):
             "gpu_matches_oracle_on_sample": match}
 
 
+def attainable_for(res, reps=20):
+    """the attainable rate of a bare non-temporal read of the same
+    frame bytes (tools/hbm_probe.hip in library form, built by `make tools`), on
+    the batch just measured: uniform aligned frames (chunk stride, data at
+    +256) or a packed (unaligned-mode) UMEM read as one span.  None for mixed
+    lengths in chunks (IMIX) or without the probe library."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "build", "libhbm_probe.so")
+    if not os.path.exists(path):
+        return None
+    lens = res["lens"]
+    n = res["n"]
+    if res["layout"] == "aligned":
+        if int(lens.min()) != int(lens.max()):
+            return None
+        chunks, stride, off, ln = n, res["chunk"] or frames.CHUNK, frames.HEADROOM, int(lens[0])
+        probe_bytes = n * ((ln + 15) // 16 * 16)
+    else:   # the packed span, as 4 KiB pieces (the probe's strides are 32-bit)
+        chunks, stride, off, ln = res["umem"].numel() // 4096, 4096, 0, 4096
+        probe_bytes = chunks * 4096
+    try:
+        lib = ctypes.CDLL(path)
+        lib.hbm_probe_read_us.restype = ctypes.c_double
+        lib.hbm_probe_read_us.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_int]
+        torch.cuda.synchronize()
+        us = lib.hbm_probe_read_us(ctypes.c_void_p(res["umem"].data_ptr()), chunks, stride, off, ln, reps)
+    except OSError:
+        return None
+    if us <= 0:
+        return None
+    gbs = probe_bytes / us / 1e3
+    out = {"read_GBps": round(gbs, 1), "probe_us": round(us, 2), "probe_bytes": probe_bytes,
+           "probe": "tools/hbm_probe.hip: non-temporal dwordx4 read of the same bytes, nothing else"}
+    k_ms = res["sum_ms"] if res["sum_ms"] is not None else (res["kernel_ms"] if res["single_kernel"] else None)
+    if k_ms:
+        # (a single-kernel shape also writes its checks in-line; the probe only reads)
+        k_gbs = res["bytes_len"] / (k_ms / 1e3) / 1e9
+        out["kernel_frame_GBps"] = round(k_gbs, 1)
+        out["kernel_vs_attainable"] = round(k_gbs / gbs, 4)
+    return out
+
+
 def traffic_for(name):
     p = os.path.join(ROOT, "profiles", f"traffic_{name}.json")
     if os.path.exists(p):
@@ -350,7 +393,8 @@ def main():
             "kernel": kernel, "alg_bytes_per_launch": alg_bytes, "kernel_us": round(k_s * 1e6, 2),
             # SURVEY.md 8(d)'s whole-step figure: sum(len + 22) / step time (both kernels)
             "step_us": round(step_k_s * 1e6, 2), "step_alg_bytes": step_alg,
-            "step_frac": round(step_alg / step_k_s / 1e9 / HBM_PEAK_GBS, 4)}
+            "step_frac": round(step_alg / step_k_s / 1e9 / HBM_PEAK_GBS, 4),
+            "attainable": attainable_for(prim)}
     cpu = None
     if rank == 0 and prim["sample"] is not None:
         cpu = cpu_baseline(prim, args.cpu_seconds, args.cpu_threads)

@@ -268,6 +268,40 @@ __global__ __launch_bounds__(256) void scatter_side(uint8_t *__restrict__ base, 
   }
 }
 
+// Library form (tools/build/libhbm_probe.so, -DHBM_PROBE_LIB): the attainable
+// non-temporal read time of bytes [off, off+len) of every `stride`-byte chunk
+// of an existing device buffer (nothing is written), average over `reps`
+// launches after 3 warm-up launches, on the null stream.  bench.py reports it
+// beside the summing kernel (roofline.attainable).  Returns microseconds, or a
+// negative value on a HIP error.
+extern "C" __attribute__((visibility("default"))) double hbm_probe_read_us(const void *base, uint64_t chunks,
+                                                                          uint32_t stride, uint32_t off,
+                                                                          uint32_t len, int reps) {
+  uint32_t *out = nullptr;
+  if (hipMalloc(&out, 4) != hipSuccess) return -1.0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 256;
+  const uint32_t ppc = (len + 15) / 16;
+  const uint64_t pieces = chunks * ppc;
+  const uint8_t *b = static_cast<const uint8_t *>(base);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int w = 0; w < 3; ++w)
+    hipLaunchKernelGGL(probe_mode<1>, dim3(cus * 8), dim3(256), 0, 0, b, pieces, ppc, stride, off, out);
+  (void)hipEventRecord(e0);
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(probe_mode<1>, dim3(cus * 8), dim3(256), 0, 0, b, pieces, ppc, stride, off, out);
+  (void)hipEventRecord(e1);
+  float ms = -1.0f;
+  const bool ok = hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(out);
+  return ok ? ms * 1e3 / reps : -1.0;
+}
+
+#ifndef HBM_PROBE_LIB
 int main(int argc, char **argv) {
   if (argc < 5) { fprintf(stderr, "usage: %s chunks stride off len [reps]\n", argv[0]); return 2; }
   const uint64_t chunks = strtoull(argv[1], 0, 0);
@@ -427,3 +461,4 @@ int main(int argc, char **argv) {
          (unsigned long long)chunks, stride, off, len, wr_check, wr_verdict, us, rd / us / 1e3);
   return 0;
 }
+#endif  // HBM_PROBE_LIB
