@@ -52,6 +52,16 @@ $(VETH): tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c $(RTLIB) oracle
 		-L$(LIBDIR) -lxsknf -Loracle/build -lcsum_oracle \
 		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread
 
+# A/B build: every kernel family and launch shape (tools/tune.py, tools/ab_libs.sh;
+# XSKNF_GPU_LIB=build/ab/libxsknf_gpu.so selects it).  Not the product.
+ABLIB := build/ab/libxsknf_gpu.so
+ab: $(ABLIB)
+$(ABLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h tools/check_inflight.py Makefile
+	@mkdir -p build/ab
+	$(HIPCC) $(HIPFLAGS) -DXSKNF_AB --cuda-device-only -S -o build/ab/checksummer-gfx950.s xsknf_amd/csrc/checksummer.hip
+	python3 tools/check_inflight.py build/ab/checksummer-gfx950.s
+	$(HIPCC) $(HIPFLAGS) -DXSKNF_AB -shared -o $@ $(SRCS)
+
 # keep the device assembly for inspection (VGPRs, instruction mix)
 asm: $(SRCS)
 	@mkdir -p build/asm
@@ -64,4 +74,4 @@ clean:
 	rm -rf $(LIBDIR) xsknf_amd/bin build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean tools
+.PHONY: all oracle asm clean tools ab

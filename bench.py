@@ -2,21 +2,32 @@
 """Device-resident throughput of the checksummer batch path (BASELINE.json metric).
 
 One step = one pass of the hot path (xsknf_packet_processor over every frame of
-one rx batch, checksummer_user.c:30-112) over a batch already resident in HBM.
-Default workload = BASELINE config 3: 1,048,576 frames of 1500 B in an aligned
-UMEM (2048 B chunks, data at +256).  Each rank processes its own batch (frames
-shard with no exchange), so `scaling` is weak and `value` is the aggregate.
+one rx batch, checksummer_user.c:30-112, as the per-frame loop of
+src/xsknf.c:654-672 calls it) over a batch already resident in HBM.
+Default workload = BASELINE config 3: 1,048,576 frames of 1500 B per GPU in an
+aligned UMEM (2048 B chunks, data at +256).  Each rank processes its own batch
+(frames shard with no exchange, as one xsknf worker per NIC queue does,
+src/xsknf.c:1046-1100), so `scaling` is weak and `value` is the aggregate.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 1500|64|imix|jumbo]
 
-For N > 1 launch with torch.distributed.run (one process per GPU, RCCL).
-Rank 0 prints ONE JSON line.
+--gpus N > 1 without a torch.distributed.run environment starts the N ranks
+itself (one process per GPU, RCCL); the parent never touches the GPU.  On a box
+with fewer than N GPUs the ranks share the devices over gloo (a rehearsal of
+the N-rank path, marked `rehearsal` in the line).  Rank 0 prints ONE JSON line.
+
+Secondary workloads (timed after the primary, reported under `secondary`):
+64 B (config 2) and config 4 -- the global 8,388,608-frame IMIX batch split
+into byte-balanced contiguous shards, one per rank (all of it on one GPU at
+N = 1, exactly config 4's 8-way split at N = 8).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,17 +39,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from xsknf_amd import Checksummer, ChecksummerOptions, frames  # noqa: E402
+from xsknf_amd.shard import shard_by_bytes  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 DESC_BYTES, VERDICT_BYTES, CHECK_BYTES = 16, 4, 2
+CONFIG4_FRAMES = 8 * (1 << 20)  # BASELINE config 4: 8,388,608 IMIX frames over the node
 
 WORKLOADS = {
     # name: (length, layout, chunk, description)
     "1500": (1500, "aligned", 2048, "BASELINE config 3: 1500 B frames, aligned UMEM 2048 B chunks, data at +256"),
     "64": (64, "aligned", 2048, "BASELINE config 2: 64 B frames, aligned UMEM 2048 B chunks, data at +256"),
-    "imix": ("imix", "aligned", 2048, "BASELINE config 4 shard: IMIX 64/570/1500 B (7:4:1), aligned 2048 B chunks"),
+    "imix": ("imix", "aligned", 2048, "IMIX 64/570/1500 B (7:4:1), 1M frames per GPU, aligned 2048 B chunks"),
     "jumbo": (9000, "unaligned", 0, "BASELINE config 5: 9000 B frames, unaligned-chunk UMEM, ~50% odd starts"),
+    "config4": ("imix", "aligned", 2048,
+                "BASELINE config 4: 8,388,608 IMIX 64/570/1500 B frames (7:4:1) split into byte-balanced "
+                "contiguous shards, one per GPU, aligned 2048 B chunks"),
 }
 
 
@@ -48,8 +64,10 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="1500", choices=sorted(WORKLOADS))
-    p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU")
-    p.add_argument("--secondary", default="64",
+    p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU (config4: global frames "
+                   f"= {CONFIG4_FRAMES} unless --config4-frames)")
+    p.add_argument("--config4-frames", type=int, default=CONFIG4_FRAMES)
+    p.add_argument("--secondary", default="64,config4",
                    help="comma list of extra workloads timed after the primary ('' = none)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
@@ -61,8 +79,37 @@ def parse():
                    help="N > 1: also time the distribution of a root-resident global IMIX batch "
                         "(SURVEY 8(e) collective 1), reported as `root_scatter`")
     p.add_argument("--kernel-steps", type=int, default=50,
-                   help="launches of the summing kernel alone for the roofline (0 = skip)")
+                   help="launches of the summing kernel alone (records only), reported beside the step")
     return p.parse_args()
+
+
+# ---- rank launch --------------------------------------------------------------
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) outside a torch.distributed.run environment: start the
+    N ranks as a child torch.distributed.run and return its exit code.  This
+    process only counts devices (torch.cuda.device_count() does not initialise
+    the GPU) and never execs: the ranks are a child process."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    env = dict(os.environ)
+    ndev = torch.cuda.device_count()
+    if ndev < args.gpus and "XSKNF_BENCH_BACKEND" not in env:
+        env["XSKNF_BENCH_BACKEND"] = "gloo"
+        print(f"bench: {args.gpus} ranks on {ndev} GPU(s): gloo rehearsal, ranks share devices",
+              file=sys.stderr)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=env)
 
 
 def dist_setup(args):
@@ -73,18 +120,21 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("XSKNF_BENCH_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
     if backend != "nccl":
-        local %= max(1, torch.cuda.device_count())
+        local %= ndev
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
-    return world, rank, torch.device("cuda", local)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
+    rehearsal = None
+    if world > 1 and backend != "nccl":
+        rehearsal = f"{backend}: {world} ranks on {min(world, ndev)} GPU(s); timings are contended, not a scaling point"
+    return world, rank, torch.device("cuda", local), rehearsal
 
 
 def barrier(world):
@@ -113,11 +163,24 @@ def allreduce_sum_i64(vals, world):
     return [int(x) for x in t.tolist()]
 
 
-def time_workload(name, args, world, rank, dev, seed):
+# ---- one workload ---------------------------------------------------------------
+
+def workload_lengths(name, args, world, rank):
+    """This rank's frame lengths (and, for config4, its [lo, hi) of the global batch)."""
+    length, layout, chunk, _ = WORKLOADS[name]
+    if name == "config4":
+        glens = frames.imix_lengths(args.config4_frames, np.random.default_rng(frames.SEED))
+        lo, hi = shard_by_bytes(glens, world)[rank]
+        return glens[lo:hi].astype(np.uint32), (lo, hi)
+    return frames._lens(args.frames, length, np.random.default_rng(frames.SEED + rank)), None
+
+
+def time_workload(name, args, world, rank, dev, seed, primary):
     length, layout, chunk, desc = WORKLOADS[name]
-    umem, descs, lens = frames.device_batch(args.frames, length, layout=layout,
-                                            chunk=chunk or frames.CHUNK, seed=seed, device=dev)
-    n = args.frames
+    lens_in, span = workload_lengths(name, args, world, rank)
+    n = int(lens_in.shape[0])
+    umem, descs, lens = frames.device_batch(n, lens_in, layout=layout, chunk=chunk or frames.CHUNK, seed=seed,
+                                            device=dev)
     hint = int(lens.max())
     cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint)
     verdicts = torch.empty(n, dtype=torch.int32, device=dev)
@@ -126,7 +189,7 @@ def time_workload(name, args, world, rank, dev, seed):
 
     # a bounded host sample of the ORIGINAL frames for the CPU baseline leg
     sample = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if primary and rank == 0 and world == 1 and args.cpu_seconds > 0:
         k = min(n, 1 << 16)
         dk = descs[:k].cpu().numpy().view(frames.DESC_DTYPE).reshape(-1)
         offs = (dk["addr"] & np.uint64((1 << 48) - 1)) + (dk["addr"] >> np.uint64(48))
@@ -157,16 +220,15 @@ def time_workload(name, args, world, rank, dev, seed):
     ev1.record(stream)
     barrier(world)
     wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps       # HIP events on the launch stream
+    step_ms = ev0.elapsed_time(ev1) / args.steps        # HIP events on the launch stream
     wall_max = allreduce_max(wall, world)
+    step_ms_max = allreduce_max(step_ms, world)
 
-    # dominant kernel alone: the summing kernel in records-only mode
-    # (include/xsknf_gpu.h fused_stores = 3), same shape, same stream, HIP
-    # events around K launches.  It only reads the UMEM, so the step's output
-    # is unaffected; for frames >= 1024 B (every frame of 1500 / jumbo) it is
-    # exactly the step's first kernel, which defers every check there too.
-    # (A single-kernel shape -- fused_stores mode 1, every check in-line -- has
-    # no second kernel: its step IS the dominant kernel.)
+    # the summing kernel alone, for reference beside the step: records-only
+    # mode (include/xsknf_gpu.h fused_stores = 3), same shape, same stream, HIP
+    # events around K launches (it only reads the UMEM).  For frames >= 1024 B
+    # it is exactly the step's first kernel; a single-kernel shape (checks
+    # in-line, fused_stores mode 1) has no second kernel: its step IS the kernel.
     import ctypes
     from xsknf_amd import _lib
     lib = _lib.load()
@@ -175,7 +237,7 @@ def time_workload(name, args, world, rank, dev, seed):
     single_kernel = (cfg.fused_stores & 3) == 1
     family = "checksum_kernel_split" if cfg.kernel == 1 else "checksum_kernel"
     k_ms = None
-    if args.kernel_steps > 0 and not single_kernel:
+    if primary and args.kernel_steps > 0 and not single_kernel:
         cfg.fused_stores = 3
         rec = torch.empty(n, dtype=torch.int32, device=dev)
         opts = cs.csum_opts()
@@ -202,11 +264,9 @@ def time_workload(name, args, world, rank, dev, seed):
     vh = verdicts.cpu().numpy()
     bytes_len = int(lens.sum())
     counters = allreduce_sum_i64([n, bytes_len, int((vh == -1).sum()), int((vh >= 0).sum())], world)
-    res = dict(name=name, desc=desc, n=n, lens=lens, bytes_len=bytes_len, kernel_ms=kernel_ms, sum_ms=k_ms,
-               single_kernel=single_kernel, family=family,
-               wall_max=wall_max, counters=counters, umem=umem, descs=descs, verdicts=verdicts,
-               sample=sample, layout=layout, chunk=chunk)
-    return res
+    return dict(name=name, desc=desc, n=n, lens=lens, bytes_len=bytes_len, step_ms=step_ms, step_ms_max=step_ms_max,
+                sum_ms=k_ms, single_kernel=single_kernel, family=family, wall_max=wall_max, counters=counters,
+                umem=umem, descs=descs, verdicts=verdicts, sample=sample, layout=layout, chunk=chunk, span=span)
 
 
 def root_scatter_leg(args, world, rank, dev):
@@ -216,7 +276,7 @@ def root_scatter_leg(args, world, rank, dev):
     span + its descriptors, point-to-point over xGMI, all ranks at once) and
     checksums it.  Reported separately from `value`: the device-resident metric
     excludes the distribution, and in the reference frames arrive per NIC queue."""
-    from xsknf_amd.shard import scatter_from_root, shard_by_bytes
+    from xsknf_amd.shard import scatter_from_root
     n_total = args.frames * world
     umem = descs = ranges = None
     if rank == 0:
@@ -266,6 +326,18 @@ def root_scatter_leg(args, world, rank, dev):
             "layout": "IMIX 64/570/1500 (7:4:1) packed, unaligned-mode descriptors; shards by bytes"}
 
 
+# ---- CPU baseline, attainable read, traffic ------------------------------------
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(res, budget_s, threads, check=True):
     """Oracle (the C restatement, gcc -O2 -flto) timed on host cores over a bounded
     sample of the same workload; also checks the GPU result on that sample."""
@@ -288,7 +360,8 @@ def cpu_baseline(res, budget_s, threads, check=True):
         g_v = res["verdicts"][:k].cpu().numpy()
         match = bool(np.array_equal(g_v, v) and np.array_equal(g_umem, umem_host))
     return {"value": round(float(gbs), 4), "unit": "GB/s checksummed", "cores": threads,
-            "kind": "port", "mpps": round(k * reps / t / 1e6, 4),
+            "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "mpps": round(k * reps / t / 1e6, 4),
             "sample": f"{k} frames of the same workload ({lens.sum() / 1e6:.1f} MB) x {reps} passes, "
                       f"{t:.1f} s, process_batch_1if-shaped loop (batch 64), 1 pinned core"
                       if threads == 1 else f"{k} frames x {reps} passes, {threads} threads",
@@ -312,24 +385,24 @@ def attainable_for(res, reps=20):
             return None
         chunks, stride, off, ln = n, res["chunk"] or frames.CHUNK, frames.HEADROOM, int(lens[0])
         probe_bytes = n * ((ln + 15) // 16 * 16)
-    else:   # the packed span, as 4 KiB pieces (the probe's strides are 32-bit)
-        chunks, stride, off, ln = res["umem"].numel() // 4096, 4096, 0, 4096
-        probe_bytes = chunks * 4096
+    else:   # the packed span
+        chunks, stride, off, ln = 1, 0, 0, res["umem"].numel() // 16 * 16
+        probe_bytes = ln
     try:
         lib = ctypes.CDLL(path)
         lib.hbm_probe_read_us.restype = ctypes.c_double
-        lib.hbm_probe_read_us.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
-                                          ctypes.c_uint32, ctypes.c_int]
+        lib.hbm_probe_read_us.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                          ctypes.c_uint64, ctypes.c_int]
         torch.cuda.synchronize()
         us = lib.hbm_probe_read_us(ctypes.c_void_p(res["umem"].data_ptr()), chunks, stride, off, ln, reps)
-    except OSError:
+    except (OSError, AttributeError):
         return None
     if us <= 0:
         return None
     gbs = probe_bytes / us / 1e3
     out = {"read_GBps": round(gbs, 1), "probe_us": round(us, 2), "probe_bytes": probe_bytes,
-           "probe": "tools/hbm_probe.hip: non-temporal dwordx4 read of the same bytes, nothing else"}
-    k_ms = res["sum_ms"] if res["sum_ms"] is not None else (res["kernel_ms"] if res["single_kernel"] else None)
+           "probe": "tools/hbm_probe.hip: fastest of its read shapes over the same bytes, nothing written"}
+    k_ms = res["sum_ms"] if res["sum_ms"] is not None else (res["step_ms"] if res["single_kernel"] else None)
     if k_ms:
         # (a single-kernel shape also writes its checks in-line; the probe only reads)
         k_gbs = res["bytes_len"] / (k_ms / 1e3) / 1e9
@@ -339,62 +412,74 @@ def attainable_for(res, reps=20):
 
 
 def traffic_for(name):
+    """HBM bytes of one step (every kernel of it) from the committed rocprofv3
+    PMC passes (tools/traffic.py -> profiles/traffic_<workload>.json), or None."""
     p = os.path.join(ROOT, "profiles", f"traffic_{name}.json")
     if os.path.exists(p):
         try:
-            d = json.load(open(p))
-            # the dominant kernel's bytes per launch (tools/traffic.py); rocprof PMC
-            # passes of an earlier run, committed under profiles/
-            return (d.get("dominant") or {}).get("hbm_bytes_per_launch")
-        except Exception:
+            return json.load(open(p)).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
             return None
     return None
 
 
+def step_summary(r, steps):
+    total_frames, total_bytes = r["counters"][0], r["counters"][1]
+    t = r["step_ms_max"] / 1e3
+    alg = total_bytes + total_frames * (DESC_BYTES + VERDICT_BYTES + CHECK_BYTES)
+    out = {"frames": total_frames, "mpps": round(total_frames / t / 1e6, 2),
+           "gbs_checksummed": round(total_bytes / t / 1e9, 2), "step_us": round(r["step_ms_max"] * 1e3, 2),
+           "step_frac": round(alg / t / 1e9 / HBM_PEAK_GBS / max(1, r.get("world", 1)), 4),
+           "wall_ms_per_step": round(r["wall_max"] / steps * 1e3, 4)}
+    if r["span"] is not None:
+        out["rank0_shard"] = list(r["span"])
+    return out
+
+
 def main():
     args = parse()
-    world, rank, dev = dist_setup(args)
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    world, rank, dev, rehearsal = dist_setup(args)
     torch.cuda.set_device(dev)
     seed = frames.SEED + rank
-    prim = time_workload(args.workload, args, world, rank, dev, seed)
+    prim = time_workload(args.workload, args, world, rank, dev, seed, primary=True)
     sec = {}
     for name in [s for s in args.secondary.split(",") if s and s != args.workload]:
-        r = time_workload(name, args, world, rank, dev, seed)
-        total_frames, total_bytes = r["counters"][0], r["counters"][1]
-        sec[name] = {"mpps": round(total_frames / (r["wall_max"] / args.steps) / 1e6, 2),
-                     "gbs_checksummed": round(total_bytes / (r["wall_max"] / args.steps) / 1e9, 2),
-                     "step_us": round(r["kernel_ms"] * 1e3, 2),
-                     "sum_kernel_us": round(r["sum_ms"] * 1e3, 2) if r["sum_ms"] else None}
+        r = time_workload(name, args, world, rank, dev, seed, primary=False)
+        r["world"] = world
+        sec[name] = step_summary(r, args.steps)
         del r
+        torch.cuda.empty_cache()
 
     root_scatter = root_scatter_leg(args, world, rank, dev) if (args.root_scatter and world > 1) else None
 
     total_frames, total_bytes, n_drop, n_fwd = prim["counters"]
-    step_s = prim["wall_max"] / args.steps
+    step_s = prim["wall_max"] / args.steps          # wall clock, max over ranks: `value`
     value = total_bytes / step_s / 1e9
     mpps = total_frames / step_s / 1e6
-    # roofline of the dominant kernel (the summing kernel), per launch on this
-    # rank: algorithmic bytes = every frame byte + its 16 B descriptor read +
-    # its 4 B record / verdict write (SURVEY.md 8(d) minus the 2 B check, which
-    # the scatter kernel writes) over its average duration from HIP events
-    step_k_s = prim["kernel_ms"] / 1e3
+    # roofline (SURVEY.md 8(d)): the whole step on this rank -- every frame byte,
+    # its 16 B descriptor read, its 4 B verdict and 2 B check writes -- over the
+    # step's HIP-event time on the launch stream (both kernels of the step)
+    step_k_s = prim["step_ms"] / 1e3
     step_alg = prim["bytes_len"] + prim["n"] * (DESC_BYTES + VERDICT_BYTES + CHECK_BYTES)
+    achieved = step_alg / step_k_s / 1e9
+    kernel_alone = None
     if prim["sum_ms"] is not None:
-        k_s = prim["sum_ms"] / 1e3
-        alg_bytes = prim["bytes_len"] + prim["n"] * (DESC_BYTES + VERDICT_BYTES)
-        kernel = f"{prim['family']} (records only, launched alone)"
-    elif prim["single_kernel"]:
-        k_s, alg_bytes, kernel = step_k_s, step_alg, f"{prim['family']} (checks in-line: the whole step)"
-    else:
-        k_s, alg_bytes, kernel = step_k_s, step_alg, "whole step (summing + scatter)"
-    achieved = alg_bytes / k_s / 1e9
+        alg_k = prim["bytes_len"] + prim["n"] * (DESC_BYTES + VERDICT_BYTES)
+        kernel_alone = {"kernel": f"{prim['family']} (records only, launched alone, back to back)",
+                        "us": round(prim["sum_ms"] * 1e3, 2), "alg_bytes": alg_k,
+                        "achieved": round(alg_k / (prim["sum_ms"] / 1e3) / 1e9, 1),
+                        "frac": round(alg_k / (prim["sum_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_for(args.workload),
-            "kernel": kernel, "alg_bytes_per_launch": alg_bytes, "kernel_us": round(k_s * 1e6, 2),
-            # SURVEY.md 8(d)'s whole-step figure: sum(len + 22) / step time (both kernels)
-            "step_us": round(step_k_s * 1e6, 2), "step_alg_bytes": step_alg,
-            "step_frac": round(step_alg / step_k_s / 1e9 / HBM_PEAK_GBS, 4),
-            "attainable": attainable_for(prim)}
+            "basis": "whole step (SURVEY.md 8(d)): sum(len + 22) per batch / HIP-event step time on the launch "
+                     "stream; traffic = FETCH_SIZE/WRITE_SIZE of every kernel of one step",
+            "kernels": (f"{prim['family']} (checks in-line)" if prim["single_kernel"]
+                        else f"{prim['family']} + scatter_checks"),
+            "alg_bytes_per_step": step_alg, "step_us": round(step_k_s * 1e6, 2),
+            "summing_kernel_alone": kernel_alone, "attainable": attainable_for(prim)}
     cpu = None
     if rank == 0 and prim["sample"] is not None:
         cpu = cpu_baseline(prim, args.cpu_seconds, args.cpu_threads)
@@ -418,9 +503,11 @@ def main():
             "roofline": roof, "cpu_baseline": cpu, "secondary": sec,
             "verdicts": {"drop": n_drop, "forward": n_fwd},
         }
+        if rehearsal:
+            out["config"]["rehearsal"] = rehearsal
         if root_scatter is not None:
             out["root_scatter"] = root_scatter
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

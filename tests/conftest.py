@@ -1,3 +1,4 @@
+import multiprocessing
 import os
 import sys
 
@@ -6,6 +7,19 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+
+# Multi-process GPU tests (ranks, the NF binary, bench.py --gpus 2) start their
+# processes from a forkserver that is launched HERE, at collection time, before
+# any test initialises the GPU: a process that has initialised the GPU must
+# never exec another program, and the forkserver's children are forked from a
+# process that never touched it.
+FORKSERVER = multiprocessing.get_context("forkserver")
+try:
+    from multiprocessing import forkserver as _fs
+    _fs.set_forkserver_preload([])
+    _fs.ensure_running()
+except (OSError, ValueError):   # pragma: no cover - platform without forkserver
+    FORKSERVER = None
 
 
 def pytest_configure(config):
@@ -17,3 +31,11 @@ def pytest_configure(config):
 def oracle_lib():
     from oracle import csum_oracle
     return csum_oracle.load()
+
+
+@pytest.fixture(scope="session")
+def clean_ctx():
+    """A multiprocessing context whose processes never inherit a GPU context."""
+    if FORKSERVER is None:
+        pytest.skip("no forkserver on this platform")
+    return FORKSERVER

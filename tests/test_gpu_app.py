@@ -1,0 +1,84 @@
+"""The checksummer NF binary (xsknf_amd/bin/checksummer) and its stats.txt contract.
+
+The reference harness starts the NF as `checksummer -i IF <mode> -- -q -i <iter>
+-c DROP` (tests/test-drop-cpu.py:79-82), sends SIGUSR1 and reads the total rx
+count from ./stats.txt (tests/test-drop-cpu.py:42-49, written by print_stats,
+examples/common/statistics.c:219-264, from int_usr, checksummer_user.c:182-185).
+Here the NF runs on emulated queues (the GPU box has no AF_XDP privileges) fed
+by its built-in generator (-G COUNT[:LEN], the shape of tests/gen-traffic.lua),
+with every rx batch checksummed by the GPU hook.  The process is started from
+the forkserver of tests/conftest.py, never from this GPU-initialised process.
+"""
+import os
+import signal
+import subprocess
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+APP = os.path.join(ROOT, "xsknf_amd", "bin", "checksummer")
+
+
+def _run_app(args, cwd, want_rx, timeout):
+    """Start the NF, poll stats.txt via SIGUSR1 until it reads want_rx, then SIGINT."""
+    p = subprocess.Popen([APP, *args], cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    stats = os.path.join(cwd, "stats.txt")
+    seen = []
+    deadline = time.time() + timeout
+    try:
+        while time.time() < deadline and p.poll() is None:
+            time.sleep(0.5)
+            p.send_signal(signal.SIGUSR1)
+            time.sleep(1.2)                   # the main loop serves the request within a second
+            if os.path.exists(stats):
+                txt = open(stats).read().strip()
+                if txt:
+                    seen.append(int(txt))
+                    if seen[-1] == want_rx:
+                        time.sleep(1.0)       # let the generator drain the last tx completions
+                        break
+    finally:
+        if p.poll() is None:
+            p.send_signal(signal.SIGINT)
+        try:
+            out, err = p.communicate(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, err = p.communicate()
+    return p.returncode, seen, out, err
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(APP):
+        pytest.fail(f"{APP} is not built (make)")
+
+
+@pytest.mark.parametrize("lib_args,app_args,count,queues,tx", [
+    # the harness's own invocation (DROP), 64 B frames
+    (["-i", "emu0"], ["-q", "-i", "1", "-c", "DROP", "-G", "20000:64"], 20000, 1, False),
+    # REDIRECT (hairpin: the generator drains the tx ring), 1500 B, two workers, big batches
+    (["-i", "emu0", "-w", "2", "-b", "256"], ["-q", "-c", "REDIRECT", "-G", "8000:1500"], 8000, 2, True),
+    # the STAGED host path, several iterations
+    (["-i", "emu0", "-b", "128"], ["-q", "-i", "3", "-c", "DROP", "-g", "STAGED", "-G", "10000:570"], 10000, 1,
+     False),
+], ids=["drop-64", "redirect-1500-w2", "staged-570"])
+def test_stats_txt_on_sigusr1(gpu, clean_ctx, tmp_path, lib_args, app_args, count, queues, tx):
+    want = count * queues
+    with clean_ctx.Pool(1) as pool:
+        rc, seen, out, err = pool.apply(_run_app, (lib_args + ["--"] + app_args, str(tmp_path), want, 120))
+    assert rc == 0, err[-2000:]
+    assert seen and seen[-1] == want, (seen, err[-2000:])
+    assert seen == sorted(seen)                       # cumulative
+    assert f"generator: {want} frames delivered" in err
+    if tx:
+        assert f"{want} transmitted" in err
+    else:
+        assert "0 transmitted" in err
+    assert out == ""                                  # -q: no stats on stdout

@@ -1,0 +1,160 @@
+"""The multi-GPU path on the GPU box (BASELINE config 4).
+
+* config 4 at full size on one GPU: the global 8,388,608-frame IMIX batch split
+  into byte-balanced contiguous shards (xsknf_amd/shard.py), each shard copied
+  into its own buffer with rebased descriptors -- exactly what a rank receives --
+  and checksummed through the C ABI; every verdict and byte equals the oracle's
+  pass over the whole batch;
+* the root distribution (scatter_from_root) with two ranks on gloo, both on
+  cuda:0, the HIP kernel run on the shards each rank received;
+* `bench.py --gpus 2` started by hand on a one-GPU box starts its two ranks
+  itself (gloo rehearsal) and reports n_gpus = 2.
+
+Processes are started from the forkserver of tests/conftest.py, never from this
+(GPU-initialised) process.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import csum_oracle as O
+from xsknf_amd import Checksummer, frames
+from xsknf_amd.shard import rebase_descs, shard_by_bytes, shard_spans
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.slow
+def test_config4_global_batch_in_byte_balanced_shards(dev):
+    """BASELINE config 4: 8,388,608 IMIX frames (1 % edge cases), split 8 ways by
+    bytes; each shard's span goes to its own buffer with rebased descriptors, as
+    scatter_from_root delivers it; the union of the shards' results is the
+    oracle's pass over the whole batch, byte for byte."""
+    n, world = 8 << 20, 8
+    umem, descs, _ = frames.device_batch(n, "imix", layout="aligned", device=dev)
+    host = umem.cpu().numpy()
+    hd = descs.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1).copy()
+    del descs
+    b = frames.HostBatch(host, hd, "aligned")
+    frames.inject_edge_cases(b, 0.01, seed=404)
+    umem.copy_(torch.from_numpy(host))
+    size = host.size
+    ranges = shard_by_bytes(hd["len"], world)
+    spans = shard_spans(hd, ranges, size)
+    sums = [int(hd["len"][lo:hi].astype(np.int64).sum()) for lo, hi in ranges]
+    assert max(sums) - min(sums) <= 2 * 1500
+    gv = np.empty(n, dtype=np.int32)
+    cs = Checksummer(frame_len_hint=1500)
+    for (lo, hi), (b0, b1) in zip(ranges, spans):
+        local = torch.empty(b1 - b0 + 16, dtype=torch.uint8, device=dev)   # a rank's receive buffer
+        local[:b1 - b0].copy_(umem[b0:b1])
+        ld = rebase_descs(hd[lo:hi], b0, size)
+        ldt = torch.from_numpy(ld.view(np.int64).reshape(-1, 2).copy()).to(dev)
+        gv[lo:hi] = cs.process_batch(local, ldt).cpu().numpy()
+        umem[b0:b1].copy_(local[:b1 - b0])
+        del local, ldt
+    torch.cuda.synchronize()
+    _, ov = O.c_time_batch(host, hd, threads=16, reps=1)      # in place over the whole batch
+    assert np.array_equal(gv, ov)
+    assert np.array_equal(umem.cpu().numpy(), host)
+    assert (ov == -1).sum() > 0 and (ov == 0).sum() > 0.98 * n
+
+
+def _scatter_rank(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    from xsknf_amd.shard import scatter_from_root
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    umem = descs = ranges = None
+    if rank == 0:
+        b = frames.unaligned_batch(6000, "imix", seed=31)
+        frames.inject_edge_cases(b, 0.05, seed=32)
+        umem, descs = torch.from_numpy(b.umem.copy()), b.descs
+        ranges = shard_by_bytes(b.descs["len"], world)
+    lu, ld, (b0, b1) = scatter_from_root(dist, umem, descs, ranges, rank, world, "cpu")
+    dev = torch.device("cuda:0")
+    lu, ld = lu.to(dev), ld.to(dev)
+    v = Checksummer(frame_len_hint=1500).process_batch(lu, ld)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), b0=b0, b1=b1, umem=lu[:b1 - b0].cpu().numpy(),
+             v=v.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_root_scatter_two_ranks_hip_kernel(dev, clean_ctx, tmp_path):
+    """scatter_from_root over gloo with two ranks on cuda:0; each rank runs the
+    HIP kernel on the shard it received; bytes and verdicts equal the oracle's
+    pass over the whole batch on the root."""
+    world, port = 2, _free_port()
+    procs = [clean_ctx.Process(target=_scatter_rank, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    b = frames.unaligned_batch(6000, "imix", seed=31)
+    frames.inject_edge_cases(b, 0.05, seed=32)
+    ranges = shard_by_bytes(b.descs["len"], world)
+    full = b.umem.copy()
+    fv = O.c_process_batch(full, b.descs)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        lo, hi = ranges[r]
+        assert np.array_equal(z["v"], fv[lo:hi]), f"rank {r} verdicts"
+        assert np.array_equal(z["umem"], full[int(z["b0"]):int(z["b1"])]), f"rank {r} bytes"
+
+
+def _run(cmd, env, timeout):
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    return p.returncode, p.stdout, p.stderr
+
+
+def test_bench_gpus_n_starts_its_ranks(dev, clean_ctx):
+    """`python bench.py --gpus 2` (no torch.distributed.run around it) starts two
+    ranks itself; on a one-GPU box they rehearse over gloo; rank 0 reports
+    n_gpus = 2 and both ranks' frames, and config 4's global batch is split
+    between them."""
+    env = dict(os.environ)
+    if torch.cuda.device_count() < 2:
+        env["XSKNF_BENCH_BACKEND"] = "gloo"
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--frames", "65536",
+           "--secondary", "config4", "--config4-frames", "131072", "--cpu-seconds", "0", "--kernel-steps", "0",
+           "--min-warmup-s", "0"]
+    with clean_ctx.Pool(1) as pool:
+        rc, out, err = pool.apply(_run, (cmd, env, 400))
+    assert rc == 0, err[-3000:]
+    line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert line["config"]["global_batch"] == 2 * 65536
+    assert line["verdicts"]["forward"] == 2 * 65536
+    assert line["secondary"]["config4"]["frames"] == 131072
+    assert line["roofline"]["frac"] > 0

@@ -5,6 +5,8 @@ the two UDP check bytes of frames that reach checksummer_user.c:108).
 Small seeded batches cover every branch of checksummer_user.c:30-112; the
 BASELINE configs run at full size (1M frames) against the threaded C oracle.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -182,10 +184,20 @@ FULL = [
 @pytest.mark.slow
 @pytest.mark.parametrize("name,n,length,layout", FULL, ids=[f[0] for f in FULL])
 def test_full_size_configs_bit_exact(dev, name, n, length, layout):
-    """BASELINE configs 2-5 at full size, every byte compared with the oracle."""
+    """BASELINE configs 2-5 at full size with 1 % edge cases mixed in (SURVEY.md
+    8(d) row 2: non-IP, non-UDP, every ihl, truncated, odd lengths, ...), every
+    verdict and byte compared with the oracle; then every well-formed frame's
+    written check passes the RFC 768/1071 receive-side verification
+    (tests/rfc1071.py), except the single-fold carry losses, which are off by
+    exactly one."""
+    from tests import rfc1071
     umem, descs, lens = frames.device_batch(n, length, layout=layout, device=dev)
     host_in = umem.cpu().numpy()
-    host_descs = descs.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1)
+    host_descs = descs.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1).copy()
+    b = frames.HostBatch(host_in, host_descs, layout)
+    edge = frames.inject_edge_cases(b, 0.01, seed=n + len(name))
+    umem.copy_(torch.from_numpy(host_in))
+    descs.copy_(torch.from_numpy(host_descs.view(np.int64).reshape(n, 2)))
     hint = int(lens.max())
     v = Checksummer(frame_len_hint=hint).process_batch(umem, descs)
     torch.cuda.synchronize()
@@ -193,29 +205,51 @@ def test_full_size_configs_bit_exact(dev, name, n, length, layout):
     gv = v.cpu().numpy()
     assert np.array_equal(gv, ov)
     assert np.array_equal(umem.cpu().numpy(), host_in)
-    # every synthetic frame is a valid UDP frame: all REDIRECT to iface 0
-    assert (gv == 0).all()
+    # the clean frames are valid UDP frames: REDIRECT to iface 0
+    clean = np.ones(n, bool)
+    clean[edge] = False
+    assert (gv[clean] == 0).all() and (gv[edge] != 0).any()
+    # RFC receive-side check of what the GPU wrote, on every well-formed frame
+    idx, V = rfc1071.verify(umem, b.frame_offsets().astype(np.int64), host_descs["len"])
+    assert idx.size > 0.98 * n
+    lost = V == 0x0001
+    assert np.all((V == 0xFFFF) | lost)
+    assert lost.mean() < {64: 0.001, 1500: 0.01, 9000: 0.05}.get(length, 0.01)
 
 
-SHAPES = [
-    # lanes_per_frame, chunks_per_lane, frames_per_group, lds_ring, fused_stores
-    (8, 1, 2, 0, 0), (8, 1, 8, 0, 1), (16, 2, 4, 0, 2), (32, 3, 4, 0, 1), (32, 3, 2, 0, 0),
+# lanes_per_frame, chunks_per_lane, frames_per_group, lds_ring, fused_stores[, kernel, window]
+PRODUCT_SHAPES = [
+    # the split kernel shapes of default_cfg() under every store mode
+    # (0 per tile, 1 in-line, 2 deferred, +4 2-byte, +8 plain sectors, +16 tail scatter)
+    (16, 2, 2, 0, 0, 1, 20), (16, 2, 2, 0, 1, 1, 20), (16, 2, 2, 0, 9, 1, 20), (16, 2, 2, 0, 5, 1, 20),
+    (16, 2, 2, 0, 0, 1, 24), (16, 2, 2, 0, 1, 1, 24), (16, 2, 2, 0, 2, 1, 24), (16, 2, 2, 0, 18, 1, 24),
+    (16, 3, 1, 0, 0, 1, 24), (16, 3, 1, 0, 1, 1, 24), (16, 3, 1, 0, 2, 1, 24), (16, 3, 1, 0, 16, 1, 24),
+    (16, 3, 1, 0, 18, 1, 24), (16, 3, 1, 0, 4, 1, 24),
+    (16, 3, 2, 0, 0, 1, 20), (16, 3, 2, 0, 2, 1, 20), (16, 3, 2, 0, 20, 1, 20), (16, 3, 2, 0, 1, 1, 20),
+    # the zero-copy host path's small-batch group shapes
+    (32, 3, 2, 0, 0), (32, 3, 2, 0, 1), (32, 3, 2, 0, 5), (64, 2, 4, 0, 2), (64, 2, 4, 0, 1),
+]
+# every other family / shape: only in the A/B build (`make ab`, XSKNF_GPU_LIB=build/ab/libxsknf_gpu.so)
+AB_SHAPES = [
+    (8, 1, 2, 0, 0), (8, 1, 8, 0, 1), (16, 2, 4, 0, 2), (32, 3, 4, 0, 1),
     (64, 9, 2, 0, 2), (64, 2, 8, 0, 0), (8, 1, 1, 3, 2), (16, 2, 1, 3, 1), (32, 3, 1, 2, 0), (32, 3, 1, 3, 1),
     (64, 4, 1, 3, 0), (64, 2, 1, 4, 1),
     (4, 2, 4, 0, 1), (4, 2, 2, 0, 0), (4, 2, 4, 0, 5),
-    # lane per frame (window 5..7 chunks; longer frames take the per-lane tail loop)
     (1, 5, 2, 0, 1), (1, 5, 4, 0, 0), (1, 6, 2, 0, 9), (1, 7, 2, 0, 5), (1, 5, 2, 0, 2),
-    # 2-byte in-line stores instead of whole-sector rewrites
     (8, 1, 4, 0, 5), (16, 2, 4, 0, 4), (32, 3, 4, 0, 5),
-    # split kernel (headers by lane, payload items by lane groups): + kernel, window
     (16, 2, 2, 0, 0, 1, 4), (16, 2, 1, 0, 1, 1, 4), (8, 4, 2, 0, 2, 1, 4), (32, 1, 2, 0, 5, 1, 4),
     (16, 4, 1, 0, 4, 1, 4), (16, 2, 2, 0, 0, 1, 5), (64, 2, 1, 0, 0, 1, 4), (32, 2, 1, 0, 1, 1, 4),
     (16, 2, 1, 0, 0, 1, 7), (16, 3, 1, 0, 2, 1, 4), (8, 2, 2, 0, 1, 1, 4),
-    (16, 2, 2, 0, 0, 1, 20), (16, 3, 1, 0, 1, 1, 20), (16, 2, 1, 0, 5, 1, 20),
-    (16, 3, 1, 0, 0, 1, 24), (16, 2, 2, 0, 1, 1, 24), (32, 3, 1, 0, 2, 1, 24), (16, 2, 1, 0, 1, 1, 24),
-    # + 16: deferred checks patched in the summing kernel's tail (no scatter launch)
-    (16, 3, 1, 0, 16, 1, 24), (16, 3, 1, 0, 18, 1, 24), (16, 2, 2, 0, 18, 1, 4), (16, 3, 2, 0, 20, 1, 20),
+    (16, 2, 1, 0, 5, 1, 20), (16, 3, 1, 0, 1, 1, 20), (16, 2, 1, 0, 1, 1, 24), (32, 3, 1, 0, 2, 1, 24),
 ]
+AB_BUILD = "ab" in os.path.basename(os.path.dirname(os.environ.get("XSKNF_GPU_LIB", "")))
+SHAPES = PRODUCT_SHAPES + [pytest.param(s, marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only"))
+                           for s in AB_SHAPES]
+
+
+def _shape_id(s):
+    s = s.values[0] if hasattr(s, "values") else s
+    return "-".join(map(str, s))
 
 
 def launch_cfg(shape, bpc=4, fused=None):
@@ -225,7 +259,7 @@ def launch_cfg(shape, bpc=4, fused=None):
                           kernel, window)
 
 
-@pytest.mark.parametrize("shape", SHAPES, ids=["-".join(map(str, s)) for s in SHAPES])
+@pytest.mark.parametrize("shape", SHAPES, ids=[_shape_id(s) for s in SHAPES])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
 def test_every_launch_shape_is_bit_exact(dev, shape, layout):
     """Each kernel family / shape / store mode, through xsknf_gpu_checksum_batch_cfg."""
@@ -254,8 +288,8 @@ def test_every_launch_shape_is_bit_exact(dev, shape, layout):
     assert np.array_equal(umem.cpu().numpy(), ou)
 
 
-@pytest.mark.parametrize("shape", [(16, 2, 4, 0), (8, 1, 4, 0), (64, 4, 1, 3), (16, 2, 2, 0, 0, 1, 4)],
-                         ids=["reg16", "reg8", "dma64", "split16"])
+@pytest.mark.parametrize("shape", [(32, 3, 2, 0), (64, 2, 4, 0), (16, 3, 1, 0, 0, 1, 24), (16, 2, 2, 0, 0, 1, 20)],
+                         ids=["reg32", "reg64", "split-w8", "split-w4"])
 def test_records_only_mode(dev, shape):
     """fused_stores = 3: the UMEM is only read; applying the records as
     include/xsknf_gpu.h documents them gives the oracle's bytes and verdicts."""
@@ -316,7 +350,7 @@ def test_host_path_bit_exact(dev, path, layout):
 
 
 @pytest.mark.parametrize("shape", [(16, 2, 2, 0, 1, 1, 20), (16, 3, 1, 0, 0, 1, 24), (16, 3, 2, 0, 2, 1, 20),
-                                   (16, 2, 1, 0, 5, 1, 4)], ids=["w4-16x2", "w8-16x3", "w4-16x3u2", "w4-lane"])
+                                   (16, 2, 2, 0, 5, 1, 24)], ids=["w4-16x2", "w8-16x3", "w4-16x3u2", "w8-16x2-2B"])
 def test_huge_frames_take_the_whole_wave_path(dev, shape):
     """Frames with more payload items than the split kernel's per-frame item
     budget (over ~27-43 KB) are summed by the whole wave; mixed in the same

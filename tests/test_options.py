@@ -1,8 +1,11 @@
-"""Host-side mirrors of the reference's option parsing: checksummer_user.c:139-175
-(app options, getopt "qxai:c:") and src/xsknf.c:777-874 (library options)."""
+"""The reference's option parsing: checksummer_user.c:139-175 (app options,
+getopt "qxai:c:", mirrored for the Python API) and src/xsknf.c:777-874 (library
+options: the runtime's C xsknf_parse_args, bound by runtime.parse_args -- one
+parser for the binary and the Python API)."""
 import pytest
 
-from xsknf_amd import ACTION_DROP, ACTION_REDIRECT, parse_args, parse_command_line
+from xsknf_amd import ACTION_DROP, ACTION_REDIRECT, parse_command_line
+from xsknf_amd import runtime as R
 
 
 def test_app_defaults_match_reference_globals():
@@ -33,25 +36,21 @@ def test_invalid_action_exits_with_usage(capsys):
 
 
 def test_library_options_and_defaults():
-    cfg, app = parse_args(["-i", "veth1b:c", "-S", "--", "-q", "-c", "DROP"])
-    assert cfg.interfaces == ["veth1b"] and cfg.bind_flags == ["copy"] and cfg.skb_mode
+    cfg, app = R.parse_args(["-i", "veth1b:c", "-S", "--", "-q", "-c", "DROP"])
+    assert cfg.num_interfaces == 1 and cfg.interfaces[0] == b"veth1b"
+    assert cfg.bind_flags[0] == R.XDP_USE_NEED_WAKEUP | R.XDP_COPY
+    assert cfg.xdp_flags & R.XDP_FLAGS_SKB_MODE and not cfg.xdp_flags & R.XDP_FLAGS_DRV_MODE
     assert cfg.batch_size == 64 and cfg.workers == 1 and cfg.xsk_frame_size == 4096   # :46-52
+    assert cfg.working_mode == R.MODE_AF_XDP
     assert app == ["-q", "-c", "DROP"]
-    cfg, _ = parse_args(["-i", "eth0:z", "-i", "eth1", "-b", "256", "-B", "-w", "4", "-u", "-f", "9000",
-                         "-M", "COMBINED", "-p"])
-    assert cfg.num_interfaces == 2 and cfg.bind_flags == ["zerocopy", ""]
+    cfg, app = R.parse_args(["-i", "eth0:z", "-i", "eth1", "-b", "256", "-B", "-w", "4", "-u", "-f", "9000",
+                             "-M", "COMBINED", "-p"])
+    assert cfg.num_interfaces == 2 and [cfg.interfaces[i] for i in range(2)] == [b"eth0", b"eth1"]
+    assert cfg.bind_flags[0] == R.XDP_USE_NEED_WAKEUP | R.XDP_ZEROCOPY and cfg.bind_flags[1] == R.XDP_USE_NEED_WAKEUP
     assert cfg.batch_size == 256 and cfg.busy_poll and cfg.workers == 4 and cfg.poll
-    assert cfg.unaligned_chunks and cfg.xsk_frame_size == 9000 and cfg.working_mode == 3
-
-
-@pytest.mark.parametrize("argv", [
-    [],                                   # no interface (:857-860)
-    ["-i", "eth0:q"],                     # unknown copy mode (:801-805)
-    ["-i", "eth0", "-M", "FAST"],         # unknown mode (:841-843)
-    ["-i", "eth0", "-w", "0"],            # workers < 1 (:846-850)
-    ["-i", "eth0", "-f", "3000"],         # non-power-of-two frame size, aligned (:866-871)
-])
-def test_library_option_errors_exit_1(argv):
-    with pytest.raises(SystemExit) as e:
-        parse_args(argv)
-    assert e.value.code == 1
+    assert cfg.unaligned_chunks and cfg.xsk_frame_size == 9000 and cfg.working_mode == R.MODE_COMBINED
+    assert cfg.xdp_flags & R.XDP_FLAGS_DRV_MODE and app == []
+    # the app's own parser takes what follows `--`, as checksummer_user.c:197 resumes getopt there
+    cfg, app = R.parse_args(["--iface=ens1f0", "--", "-i", "5", "-c", "DROP"])
+    o = parse_command_line(app)
+    assert cfg.interfaces[0] == b"ens1f0" and o.csum_iterations == 5 and o.action == ACTION_DROP

@@ -19,7 +19,6 @@ import numpy as np
 import pytest
 
 from oracle import csum_oracle as O
-from xsknf_amd import checksummer as C
 from xsknf_amd import runtime as R
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -217,25 +216,31 @@ def _c_parse(argv):
     return cfg, names
 
 
-@pytest.mark.parametrize("argv", [
-    ["nf", "-i", "eth0"],
-    ["nf", "-i", "eth0:c", "-i", "eth1:z", "-S", "-b", "128", "-w", "2", "-p"],
-    ["nf", "--iface=ens1f0", "--unaligned", "--frame-size=3000", "--busy-poll", "-M", "AF_XDP"],
-    ["nf", "-i", "veth0", "-f", "2048", "--", "-c", "DROP", "-i", "5"],
+@pytest.mark.parametrize("argv,want", [
+    (["nf", "-i", "eth0"], dict(names=["eth0"], workers=1, batch=64, poll=0, busy=0, unaligned=0, fs=4096,
+                                skb=False, bind=[""])),
+    (["nf", "-i", "eth0:c", "-i", "eth1:z", "-S", "-b", "128", "-w", "2", "-p"],
+     dict(names=["eth0", "eth1"], workers=2, batch=128, poll=1, busy=0, unaligned=0, fs=4096, skb=True,
+          bind=["copy", "zerocopy"])),
+    (["nf", "--iface=ens1f0", "--unaligned", "--frame-size=3000", "--busy-poll", "-M", "AF_XDP"],
+     dict(names=["ens1f0"], workers=1, batch=64, poll=0, busy=1, unaligned=1, fs=3000, skb=False, bind=[""])),
+    (["nf", "-i", "veth0", "-f", "2048", "--", "-c", "DROP", "-i", "5"],
+     dict(names=["veth0"], workers=1, batch=64, poll=0, busy=0, unaligned=0, fs=2048, skb=False, bind=[""])),
 ])
-def test_parse_args_matches_the_python_mirror(argv):
-    cfg, names = _c_parse(argv)
-    py, _ = C.parse_args(argv[1:])
-    assert names == py.interfaces
-    assert cfg.workers == py.workers and cfg.batch_size == py.batch_size
-    assert bool(cfg.poll) == py.poll and bool(cfg.busy_poll) == py.busy_poll
-    assert bool(cfg.unaligned_chunks) == py.unaligned_chunks and cfg.xsk_frame_size == py.xsk_frame_size
-    assert bool(cfg.xdp_flags & R.XDP_FLAGS_SKB_MODE) == py.skb_mode
-    assert cfg.xdp_flags & R.XDP_FLAGS_DRV_MODE == (0 if py.skb_mode else R.XDP_FLAGS_DRV_MODE)
-    for i, mode in enumerate(py.bind_flags):
-        want = R.XDP_USE_NEED_WAKEUP | {"": 0, "copy": R.XDP_COPY, "zerocopy": R.XDP_ZEROCOPY}[mode]
-        assert cfg.bind_flags[i] == want
-    assert cfg.ebpf_filename == b"nf_kern.o" and cfg.xdp_progname == b"handle_xdp"
+def test_parse_args_defaults_and_options(argv, want):
+    """src/xsknf.c:777-874 (defaults :46-52), and runtime.parse_args binding the same C parser."""
+    bound, _ = R.parse_args(argv[1:], prog="nf")
+    for cfg, names in (_c_parse(argv), (bound, [bound.interfaces[i].decode() for i in range(bound.num_interfaces)])):
+        assert names == want["names"]
+        assert cfg.workers == want["workers"] and cfg.batch_size == want["batch"]
+        assert cfg.poll == want["poll"] and cfg.busy_poll == want["busy"]
+        assert cfg.unaligned_chunks == want["unaligned"] and cfg.xsk_frame_size == want["fs"]
+        assert bool(cfg.xdp_flags & R.XDP_FLAGS_SKB_MODE) == want["skb"]
+        assert cfg.xdp_flags & R.XDP_FLAGS_DRV_MODE == (0 if want["skb"] else R.XDP_FLAGS_DRV_MODE)
+        for i, mode in enumerate(want["bind"]):
+            wantf = R.XDP_USE_NEED_WAKEUP | {"": 0, "copy": R.XDP_COPY, "zerocopy": R.XDP_ZEROCOPY}[mode]
+            assert cfg.bind_flags[i] == wantf
+        assert cfg.ebpf_filename == b"nf_kern.o" and cfg.xdp_progname == b"handle_xdp"
 
 
 @pytest.mark.parametrize("argv", [["nf"], ["nf", "-i", "eth0:x"], ["nf", "-i", "e0", "-M", "FOO"],

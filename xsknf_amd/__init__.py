@@ -5,8 +5,8 @@ AF_XDP frame; here a whole rx batch is checksummed by one gfx950 kernel
 (`xsknf_amd/csrc/checksummer.hip`) behind the C ABI of `include/xsknf_gpu.h`.
 """
 from .checksummer import (ACTION_DROP, ACTION_REDIRECT, Checksummer, ChecksummerOptions, HostPath,
-                          XsknfConfig, parse_args, parse_command_line)
+                          parse_command_line)
 
 __all__ = ["ACTION_DROP", "ACTION_REDIRECT", "Checksummer", "ChecksummerOptions", "HostPath",
-           "XsknfConfig", "parse_args", "parse_command_line"]
+           "parse_command_line"]
 __version__ = "0.1.0"

@@ -5,9 +5,8 @@ Reference: examples/checksummer/checksummer_user.c
   * opt_action / opt_csum_iterations                    :24-25
   * xsknf_packet_processor(pkt, len, ingress_ifindex)   :30-112 (per frame)
   * parse_command_line(), getopt "qxai:c:"              :139-175
-and the library option parser src/xsknf.c:777-874 (xsknf_parse_args, getopt
-"i:pSf:ub:BM:w:"), whose frame size / unaligned / batch size decide the UMEM
-layout the batch path reads.
+(The library options, src/xsknf.c:777-874, are parsed by the runtime's own C
+xsknf_parse_args(): runtime.parse_args() binds it; there is one parser.)
 
 The per-frame callback becomes `Checksummer.process_batch()`: one call per rx
 batch, device-resident UMEM + descriptors, verdicts with the callback's meaning
@@ -19,19 +18,13 @@ from __future__ import annotations
 import ctypes
 import getopt
 import sys
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import List, Optional
 
 from . import _lib
 
 ACTION_REDIRECT = _lib.ACTION_REDIRECT
 ACTION_DROP = _lib.ACTION_DROP
-XSKNF_MAX_INTERFACES = 32          # src/xsknf.h:11
-XSKNF_MAX_WORKERS = 32             # src/xsknf.h:12
-MODE_AF_XDP = 0x1                  # src/xsknf.h:15-17
-MODE_XDP = 0x2
-MODE_COMBINED = MODE_AF_XDP | MODE_XDP
-XSK_UMEM_DEFAULT_FRAME_SIZE = 4096  # libxdp default (src/xsknf.c:48)
 
 _APP_USAGE = (
     "  Usage: %s [XSKNF_OPTIONS] -- [APP_OPTIONS]\n"
@@ -106,84 +99,6 @@ def parse_command_line(argv: List[str], prog: str = "checksummer") -> Checksumme
         elif k in ("-a", "--app-stats"):
             o.app_stats = True
     return o
-
-
-@dataclass
-class XsknfConfig:
-    """struct xsknf_config (src/xsknf.h:25-40) with the defaults of src/xsknf.c:46-52."""
-    interfaces: List[str] = field(default_factory=list)
-    bind_flags: List[str] = field(default_factory=list)   # "", "copy" or "zerocopy"
-    workers: int = 1
-    working_mode: int = MODE_AF_XDP
-    skb_mode: bool = False
-    batch_size: int = 64
-    poll: bool = False
-    unaligned_chunks: bool = False
-    xsk_frame_size: int = XSK_UMEM_DEFAULT_FRAME_SIZE
-    busy_poll: bool = False
-
-    @property
-    def num_interfaces(self) -> int:
-        return len(self.interfaces)
-
-
-def parse_args(argv: List[str]) -> tuple:
-    """Mirror of xsknf_parse_args (src/xsknf.c:777-874): returns (config, app_argv).
-
-    Errors follow the reference: unknown copy mode / mode / workers < 1 / no
-    interface / non-power-of-two frame size in aligned mode -> message + exit(1)."""
-    cfg = XsknfConfig()
-    if "--" in argv:
-        cut = argv.index("--")
-        lib_argv, app_argv = argv[:cut], argv[cut + 1:]
-    else:
-        lib_argv, app_argv = argv, []
-    try:
-        opts, _ = getopt.getopt(lib_argv, "i:pSf:ub:BM:w:",
-                                ["iface=", "poll", "xdp-skb", "frame-size=", "unaligned",
-                                 "batch-size=", "busy-poll", "mode=", "workers="])
-    except getopt.GetoptError as e:
-        sys.stderr.write(f"ERROR: {e}\n")
-        sys.exit(1)
-    for k, v in opts:
-        if k in ("-i", "--iface"):
-            name, _, mode = v.partition(":")
-            if mode and mode not in ("c", "z"):
-                sys.stderr.write(f"ERROR: unknown copy mode '{mode[0]}'\n")
-                sys.exit(1)
-            cfg.interfaces.append(name)
-            cfg.bind_flags.append({"": "", "c": "copy", "z": "zerocopy"}[mode[:1]])
-        elif k in ("-p", "--poll"):
-            cfg.poll = True
-        elif k in ("-S", "--xdp-skb"):
-            cfg.skb_mode = True
-        elif k in ("-u", "--unaligned"):
-            cfg.unaligned_chunks = True
-        elif k in ("-f", "--frame-size"):
-            cfg.xsk_frame_size = _atoi(v)
-        elif k in ("-b", "--batch-size"):
-            cfg.batch_size = _atoi(v)
-        elif k in ("-B", "--busy-poll"):
-            cfg.busy_poll = True
-        elif k in ("-M", "--mode"):
-            m = {"AF_XDP": MODE_AF_XDP, "XDP": MODE_XDP, "COMBINED": MODE_COMBINED}.get(v)
-            if m is None:
-                sys.stderr.write(f"ERROR: unknown working mode {v}\n")
-                sys.exit(1)
-            cfg.working_mode = m
-        elif k in ("-w", "--workers"):
-            cfg.workers = _atoi(v)
-            if cfg.workers < 1:
-                sys.stderr.write(f"ERROR: Invalid number of workers {cfg.workers}")
-                sys.exit(1)
-    if not cfg.interfaces:
-        sys.stderr.write("ERROR: at least one interface in required\n")
-        sys.exit(1)
-    fs = cfg.xsk_frame_size
-    if (fs & (fs - 1)) and not cfg.unaligned_chunks:
-        sys.stderr.write(f"--frame-size={fs} is not a power of two\n")
-        sys.exit(1)
-    return cfg, app_argv
 
 
 class Checksummer:

@@ -40,6 +40,7 @@
 //   scatter pass then writes the 2 check bytes per frame and the verdicts.
 #include <hip/hip_runtime.h>
 #include <atomic>
+#include <mutex>
 #include <stdint.h>
 #include <errno.h>
 #include <stdio.h>
@@ -53,7 +54,7 @@ namespace xsknf_gpu {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kTile = 64;        // consecutive frames per wave tile (one 256-B result store)
+[[maybe_unused]] constexpr int kTile = 64;   // consecutive frames per wave tile (LDS-DMA kernel, A/B)
 constexpr int kHdrChunks = 7;    // window chunks 0..6 hold frame bytes [0, 97) at any 16-B phase
 constexpr int kSlotBytes = 128;  // register kernel: per-group LDS header window
 
@@ -697,6 +698,7 @@ __device__ __forceinline__ FrameRef lane_ref(const KernelArgs &a, const uint4 d,
   return make_ref(a, (static_cast<uint64_t>(d.y) << 32) | d.x, d.z, f < a.n);
 }
 
+#ifdef XSKNF_AB
 template <int NCH, int SPT>
 __global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs args) {
   constexpr uint32_t T = SPT * kWave;        // frames per tile
@@ -741,6 +743,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs 
   }
   publish_records(args, nrec, lane);
 }
+#endif  // XSKNF_AB
 
 // ---- split kernel: headers by lane, payload by group ----------------------------
 //
@@ -1159,6 +1162,7 @@ void checksum_kernel_split(const KernelArgs args) {
   }
 }
 
+#ifdef XSKNF_AB
 // ---- LDS-DMA ring kernel ------------------------------------------------------
 //
 // Each wave streams its steps (G frames, one per group) through a private ring
@@ -1284,6 +1288,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs a
     }
   }
 }
+#endif  // XSKNF_AB
 
 // ---- phase 2: write-only pass of the parked checks (:108) and verdicts -------
 //
@@ -1421,12 +1426,28 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
 
 // ---- host side ----------------------------------------------------------------
 
-thread_local char g_last_error[256] = "";
+// The last error of ANY thread: a worker thread's failure (hook context
+// creation, UMEM registration, a launch) must be readable by the application's
+// main thread (checksummer_app.c prints it).  Each reader gets a private copy,
+// so the returned text cannot change under it.
+std::mutex g_err_mu;
+char g_last_error[256] = "";
+thread_local char g_err_copy[256] = "";
 
-void set_error_text(const char *text) { snprintf(g_last_error, sizeof(g_last_error), "%s", text); }
+void set_error_text(const char *text) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  snprintf(g_last_error, sizeof(g_last_error), "%s", text);
+}
 
 void set_error(hipError_t e, const char *where) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
   snprintf(g_last_error, sizeof(g_last_error), "%s: %s", where, hipGetErrorString(e));
+}
+
+const char *last_error_copy() {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  memcpy(g_err_copy, g_last_error, sizeof(g_err_copy));
+  return g_err_copy;
 }
 
 int device_cus() {
@@ -1490,12 +1511,14 @@ int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel launch");
 }
 
+#ifdef XSKNF_AB
 template <int NCH, int SPT>
 int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   auto k = checksum_kernel_lane<NCH, SPT>;
   hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, SPT * kWave)), dim3(kBlock), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
+#endif
 
 template <int W, int LPF, int NCH, int U, bool TL>
 int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
@@ -1504,12 +1527,14 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel_split launch");
 }
 
+#ifdef XSKNF_AB
 template <int LPF, int NCH, int R>
 int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   auto k = checksum_kernel_dma<LPF, NCH, R>;
   hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kTile)), dim3(kBlock), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_dma launch");
 }
+#endif
 
 // Instantiated launch shapes: {lanes per frame, 16-B chunks per lane and pass,
 // frames per group and step (register) / items per group in flight (split),
@@ -1526,21 +1551,27 @@ struct Variant {
 // split: window field = W, + 16 for the transposed (coalesced) window load
 #define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
 const Variant kVariants[] = {
+    // the product's shapes: default_cfg()'s split kernels, one per size class ...
+    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
+    // ... and the zero-copy host path's small-batch group shapes (host_path.hip)
+    XSKNF_V(32, 3, 2), XSKNF_V(64, 2, 4),
+#ifdef XSKNF_AB
+    // A/B material (`make ab` -> build/ab/libxsknf_gpu.so; tools/tune.py), not in the product library
     XSKNF_S(4, 16, 2, 2, 0), XSKNF_S(4, 16, 2, 1, 0), XSKNF_S(4, 8, 4, 2, 0), XSKNF_S(4, 32, 1, 2, 0),
     XSKNF_S(4, 16, 4, 1, 0), XSKNF_S(5, 16, 2, 2, 0), XSKNF_S(4, 64, 2, 1, 0), XSKNF_S(4, 32, 2, 1, 0),
     XSKNF_S(7, 16, 2, 1, 0), XSKNF_S(4, 16, 3, 1, 0), XSKNF_S(4, 8, 2, 2, 0),
-    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
+    XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
-    XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 32, 3, 1, 1),
-    XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
+    XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
     XSKNF_L(5, 2),     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
-    XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 2), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
-    XSKNF_V(64, 2, 4), XSKNF_V(64, 2, 8), XSKNF_V(64, 4, 4), XSKNF_V(64, 9, 2), XSKNF_V(64, 9, 4),
+    XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
+    XSKNF_V(64, 2, 8), XSKNF_V(64, 4, 4), XSKNF_V(64, 9, 2), XSKNF_V(64, 9, 4),
     XSKNF_D(8, 1, 3),  XSKNF_D(8, 1, 4),  XSKNF_D(16, 1, 3), XSKNF_D(16, 2, 3), XSKNF_D(32, 2, 3),
     XSKNF_D(32, 3, 2), XSKNF_D(32, 3, 3), XSKNF_D(64, 2, 3), XSKNF_D(64, 2, 4), XSKNF_D(64, 3, 3),
     XSKNF_D(64, 4, 2), XSKNF_D(64, 4, 3),
+#endif
 };
 #undef XSKNF_V
 #undef XSKNF_L
@@ -1654,7 +1685,7 @@ int xsknf_gpu_device_count(int *count) {
   return 0;
 }
 
-const char *xsknf_gpu_last_error(void) { return xsknf_gpu::g_last_error; }
+const char *xsknf_gpu_last_error(void) { return xsknf_gpu::last_error_copy(); }
 
 int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
                              uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,

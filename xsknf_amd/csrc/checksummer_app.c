@@ -8,7 +8,11 @@
 // (checksummer_user.c:30-112) is replaced by the GPU batch hook of
 // libxsknf_gpu: every rx batch is checksummed by one gfx950 launch.
 //
-// Extra app option: -g, --gpu-path=ZEROCOPY|STAGED (include/xsknf_gpu.h).
+// Extra app options: -g, --gpu-path=ZEROCOPY|STAGED (include/xsknf_gpu.h);
+// -G, --emu-gen=COUNT[:LEN]: with emulated queues (interfaces "emu<k>", whose
+// kernel side lives in this process) a generator thread plays the reference
+// harness's traffic generator (tests/gen-traffic.lua): COUNT UDP frames of LEN
+// bytes (default 64) in its shape per queue, and it drains the tx rings.
 // MODE_XDP / MODE_COMBINED need the NF's eBPF object and are not supported.
 #define _GNU_SOURCE
 
@@ -16,6 +20,8 @@
 #include <getopt.h>
 #include <libgen.h>
 #include <locale.h>
+#include <pthread.h>
+#include <stdint.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -32,6 +38,8 @@ static int opt_action = XSKNF_CSUM_ACTION_REDIRECT;
 static int opt_csum_iterations = 1;
 static int opt_quiet, opt_extra_stats, opt_app_stats;
 static int opt_gpu_path = XSKNF_GPU_PATH_ZEROCOPY;
+static unsigned long opt_gen_count;
+static unsigned opt_gen_len = 64;
 static volatile sig_atomic_t benchmark_done, stats_requested;
 static struct xsknf_config config;
 
@@ -42,6 +50,7 @@ static const struct option long_options[] = {
 	{"extra-stats", no_argument, 0, 'x'},
 	{"app-stats", no_argument, 0, 'a'},
 	{"gpu-path", required_argument, 0, 'g'},
+	{"emu-gen", required_argument, 0, 'G'},
 	{0, 0, 0, 0},
 };
 
@@ -56,6 +65,7 @@ static void usage(const char *prog)
 		"  -x, --extra-stats	Display extra statistics.\n"
 		"  -a, --app-stats	Display application (syscall) statistics.\n"
 		"  -g, --gpu-path	ZEROCOPY (default) or STAGED host path to the GPU.\n"
+		"  -G, --emu-gen		COUNT[:LEN] frames per emulated queue from a built-in generator.\n"
 		"\n",
 		prog);
 	exit(EXIT_FAILURE);
@@ -64,7 +74,7 @@ static void usage(const char *prog)
 static void parse_command_line(int argc, char **argv, char *app_path)
 {
 	int option_index, c;
-	while ((c = getopt_long(argc, argv, "qxai:c:g:", long_options, &option_index)) != -1) {
+	while ((c = getopt_long(argc, argv, "qxai:c:g:G:", long_options, &option_index)) != -1) {
 		switch (c) {
 		case 'c':
 			if (!strcmp(optarg, "REDIRECT")) {
@@ -98,10 +108,101 @@ static void parse_command_line(int argc, char **argv, char *app_path)
 				usage(basename(app_path));
 			}
 			break;
+		case 'G': {
+			char *end = NULL;
+			opt_gen_count = strtoul(optarg, &end, 10);
+			if (end && *end == ':')
+				opt_gen_len = (unsigned)strtoul(end + 1, NULL, 10);
+			if (opt_gen_len < 42 || opt_gen_len > 3840) {
+				fprintf(stderr, "ERROR: invalid generator frame length %u\n", opt_gen_len);
+				usage(basename(app_path));
+			}
+			break;
+		}
 		default:
 			usage(basename(app_path));
 		}
 	}
+}
+
+/* ---- generator for emulated queues (the harness's tests/gen-traffic.lua) ---- */
+
+static unsigned long gen_delivered, gen_transmitted;
+
+// Eth 0a:00:00:00:00:01 -> 0a:00:00:00:00:00, IPv4 10.0.0.x -> 172.0.0.1 (ihl 5,
+// proto 17), UDP 5000 -> 80, random payload (gen-traffic.lua:16,92-100; the
+// checksum is left for the NF, which overwrites it).
+static void gen_frame(uint8_t *f, unsigned len, uint64_t *rng)
+{
+	static const uint8_t hdr[42] = {
+		0x0a, 0, 0, 0, 0, 0, 0x0a, 0, 0, 0, 0, 1, 0x08, 0x00,
+		0x45, 0, 0, 0, 0, 0, 0, 0, 64, 17, 0, 0, 10, 0, 0, 0, 172, 0, 0, 1,
+		0x13, 0x88, 0x00, 0x50, 0, 0, 0, 0,
+	};
+	for (unsigned i = 42; i < len; i++) {
+		*rng ^= *rng << 13;
+		*rng ^= *rng >> 7;
+		*rng ^= *rng << 17;
+		f[i] = (uint8_t)*rng;
+	}
+	memcpy(f, hdr, 42);
+	f[16] = (uint8_t)((len - 14) >> 8);
+	f[17] = (uint8_t)(len - 14);
+	f[29] = (uint8_t)*rng;          // one of 256 flows
+	f[38] = (uint8_t)((len - 34) >> 8);
+	f[39] = (uint8_t)(len - 34);
+}
+
+static void *gen_loop(void *arg)
+{
+	(void)arg;
+	enum { BURST = 256, TXSTRIDE = 4096 };
+	const unsigned queues = config.workers * config.num_interfaces;
+	uint8_t *buf = malloc((size_t)BURST * opt_gen_len);
+	uint32_t *lens = malloc(sizeof(uint32_t) * BURST);
+	uint8_t *txbuf = malloc((size_t)BURST * TXSTRIDE);
+	uint32_t *txlens = malloc(sizeof(uint32_t) * BURST);
+	unsigned long *left = calloc(queues, sizeof(unsigned long));
+	if (!buf || !lens || !txbuf || !txlens || !left)
+		goto out;
+	for (unsigned q = 0; q < queues; q++)
+		left[q] = opt_gen_count;
+	uint64_t rng = 0x58534B4EULL;
+	unsigned long pending = opt_gen_count * queues;
+	while (!benchmark_done) {
+		int idle = 1;
+		for (unsigned q = 0; q < queues; q++) {
+			const unsigned w = q / config.num_interfaces, j = q % config.num_interfaces;
+			if (left[q]) {
+				const uint32_t n = left[q] < BURST ? (uint32_t)left[q] : BURST;
+				for (uint32_t i = 0; i < n; i++) {
+					gen_frame(buf + (size_t)i * opt_gen_len, opt_gen_len, &rng);
+					lens[i] = opt_gen_len;
+				}
+				const int got = xsknf_emu_deliver(w, j, buf, lens, n, opt_gen_len);
+				if (got < 0)
+					goto out;
+				left[q] -= (unsigned)got;
+				pending -= (unsigned)got;
+				__atomic_add_fetch(&gen_delivered, (unsigned long)got, __ATOMIC_RELAXED);
+				idle &= got == 0;
+			}
+			const int sent = xsknf_emu_transmit(w, j, txbuf, txlens, BURST, TXSTRIDE);
+			if (sent > 0) {
+				__atomic_add_fetch(&gen_transmitted, (unsigned long)sent, __ATOMIC_RELAXED);
+				idle = 0;
+			}
+		}
+		if (idle)
+			usleep(pending ? 50 : 1000);
+	}
+out:
+	free(buf);
+	free(lens);
+	free(txbuf);
+	free(txlens);
+	free(left);
+	return NULL;
 }
 
 /* ---- statistics (examples/common/statistics.c:33-260) ---- */
@@ -238,6 +339,10 @@ int main(int argc, char **argv)
 		return EXIT_FAILURE;
 	}
 	prev_time = get_nsecs();
+	pthread_t gen;
+	int gen_started = 0;
+	if (opt_gen_count)
+		gen_started = pthread_create(&gen, NULL, gen_loop, NULL) == 0;
 
 	int err = 0;
 	while (!benchmark_done && !err) {
@@ -253,6 +358,12 @@ int main(int argc, char **argv)
 	}
 	if (err)
 		fprintf(stderr, "ERROR: worker stopped: %s (%s)\n", strerror(-err), xsknf_gpu_last_error());
+	benchmark_done = 1;
+	if (gen_started) {
+		pthread_join(gen, NULL);
+		fprintf(stderr, "generator: %lu frames delivered, %lu transmitted\n", gen_delivered,
+			gen_transmitted);
+	}
 	xsknf_stop_workers();
 	xsknf_gpu_hook_destroy(hook);
 	xsknf_cleanup();

@@ -499,18 +499,31 @@ static void rx_empty(struct xsk_sock *s)
 	}
 }
 
+static int recycle_pkts(struct xsk_sock *s, const struct pkt_info *p, uint32_t n)
+{
+	uint32_t idx;
+	if (!n)
+		return 0;
+	if (reserve_exact(&s->fq, n, &idx))
+		return -ENOSPC;
+	for (uint32_t i = 0; i < n; i++)
+		*ring_addr(&s->fq, idx + i) = p[i].addr;
+	ring_submit(&s->fq, n);
+	return 0;
+}
+
 static int recycle_drops(struct xsk_sock *s, uint32_t ndrop)
 {
-	struct worker *w = s->worker;
-	uint32_t idx;
-	if (!ndrop)
-		return 0;
-	if (reserve_exact(&s->fq, ndrop, &idx))
-		return -ENOSPC;
-	for (uint32_t i = 0; i < ndrop; i++)
-		*ring_addr(&s->fq, idx + i) = w->to_drop[i].addr;
-	ring_submit(&s->fq, ndrop);
-	return 0;
+	return recycle_pkts(s, s->worker->to_drop, ndrop);
+}
+
+// A stop (or a worker error) while the tx ring is full: the frames that were to
+// be sent go back to the rx socket's fill ring, so no frame leaks from the
+// socket's budget and the sockets can run again after xsknf_start_workers().
+static int abandon_tx(struct xsk_sock *rx, const struct pkt_info *p, uint32_t n)
+{
+	const int rc = recycle_pkts(rx, p, n);
+	return rx->worker->err ? rx->worker->err : rc;
 }
 
 // process_batch_1if (src/xsknf.c:630-714)
@@ -551,7 +564,7 @@ static int process_batch_1if(struct xsk_sock *s)
 				kick_tx(s);
 			}
 			if (w->err || __atomic_load_n(&stop_flag, __ATOMIC_RELAXED))
-				return w->err;
+				return abandon_tx(s, w->to_tx, ntx);
 		}
 		for (uint32_t i = 0; i < ntx; i++) {
 			struct xdp_desc *d = ring_desc(&s->tx, idx + i);
@@ -604,14 +617,33 @@ static int process_batch(struct xsk_sock *xsks, unsigned ifindex)
 			continue;
 		struct xsk_sock *tx = &xsks[i];
 		while (ring_reserve(&tx->tx, n, &idx) != n) {
+			// reap the rx interface's completions (as src/xsknf.c:554 does) and
+			// the destination's own: with its completion ring full the kernel
+			// cannot consume its tx ring, and the wait would never end
 			if ((rc = complete_tx(xsks, ifindex)))
+				return rc;
+			if (i != ifindex && (rc = complete_tx(xsks, i)))
 				return rc;
 			if (conf.busy_poll || ring_needs_wakeup(&tx->tx)) {
 				tx->stats.tx_wakeup_sendtos++;
 				kick_tx(tx);
 			}
-			if (w->err || __atomic_load_n(&stop_flag, __ATOMIC_RELAXED))
-				return w->err;
+			if (w->err || __atomic_load_n(&stop_flag, __ATOMIC_RELAXED)) {
+				// this destination's frames and every later one's, each to
+				// its owner's fill ring (as complete_tx recycles them)
+				for (unsigned k = i; k < nif; k++) {
+					const struct pkt_info *p = &w->to_tx[k * conf.batch_size];
+					for (uint32_t j = 0; j < w->ntx[k]; j++) {
+						uint64_t owner = addr_offset(p[j].addr) / socket_span;
+						if (owner >= nif)
+							owner = ifindex;
+						const int r2 = recycle_pkts(&xsks[owner], &p[j], 1);
+						if (r2 && !rc)
+							rc = r2;
+					}
+				}
+				return w->err ? w->err : rc;
+			}
 		}
 		const struct pkt_info *p = &w->to_tx[i * conf.batch_size];
 		for (uint32_t j = 0; j < n; j++) {

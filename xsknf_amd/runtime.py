@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -110,6 +110,27 @@ def load() -> ctypes.CDLL:
 def _check(rc: int, what: str) -> None:
     if rc != 0:
         raise RuntimeError_(f"{what} failed: rc={rc} ({os.strerror(-rc) if rc < 0 else rc})")
+
+
+def parse_args(argv: Sequence[str], prog: str = "checksummer") -> Tuple[Config, List[str]]:
+    """The runtime's own C xsknf_parse_args() (the reference's src/xsknf.c:777-874,
+    getopt "i:pSf:ub:BM:w:" up to `--`): returns the struct xsknf_config and the
+    application's arguments after `--`.  As in the reference, an invalid option
+    prints the error and the usage and calls exit(1): the whole process ends."""
+    lib = load()
+    args = [prog, *argv]
+    bufs = [ctypes.create_string_buffer(a.encode()) for a in args]
+    arr = (ctypes.c_char_p * (len(args) + 1))()
+    for i, b in enumerate(bufs):
+        arr[i] = ctypes.cast(b, ctypes.c_char_p)
+    libc = ctypes.CDLL(None)
+    ctypes.c_int.in_dll(libc, "optind").value = 0        # glibc: full getopt re-initialisation
+    cfg = Config()
+    _check(lib.xsknf_parse_args(len(args), arr, ctypes.byref(cfg)), "xsknf_parse_args")
+    cfg._argv_bufs = bufs                               # cfg.interfaces points into them
+    optind = ctypes.c_int.in_dll(libc, "optind").value
+    app = [arr[i].decode() for i in range(optind, len(args))]
+    return cfg, app
 
 
 def make_config(interfaces: Sequence[str], *, workers: int = 1, batch_size: int = 64,
