@@ -165,13 +165,23 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *   XSKNF_GPU_PATH_ZEROCOPY  the UMEM is pinned and mapped; the kernel reads
  *                            the frames and writes the check bytes in place
  *                            over PCIe (no copies).
- *   XSKNF_GPU_PATH_STAGED    the byte span of each batch is copied to a device
- *                            mirror (hipMemcpyAsync from the pinned UMEM) and
+ *   XSKNF_GPU_PATH_STAGED    only the batch's frame bytes are copied to a device
+ *                            mirror (merged runs, one 2-D copy for frames at a
+ *                            constant stride, or a CPU gather into a pinned
+ *                            staging buffer for scattered frames) and
  *                            checksummed in HBM; only the 4-byte records come
  *                            back and the host writes the 2 check bytes.
- * One context = one worker thread = one HIP stream.  Calls are synchronous:
- * when xsknf_gpu_ctx_process_batch() returns, verdicts and check bytes are in
- * host memory.
+ * One context = one worker thread.  It keeps two batches in flight (two slots,
+ * each with its own HIP stream): the copies and kernel of one overlap the
+ * other's, and the host's share of one overlaps the device's share of the other.
+ * xsknf_gpu_ctx_process_batch() is synchronous: when it returns, verdicts and
+ * check bytes are in host memory (a batch larger than 65536 frames runs as
+ * pieces through both slots).  xsknf_gpu_ctx_submit() returns once the batch
+ * is enqueued, with a ticket; xsknf_gpu_ctx_wait(ticket) returns once that
+ * batch and every earlier one is complete (verdicts written, check bytes in
+ * the UMEM).  A submit may itself complete older batches to free a slot.  The
+ * frames of batches in flight must not be touched by the caller, and
+ * `verdicts` must stay valid, until their wait.
  */
 #define XSKNF_GPU_PATH_ZEROCOPY 0
 #define XSKNF_GPU_PATH_STAGED 1
@@ -192,6 +202,10 @@ XSKNF_GPU_API int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *ctx, void *u
 XSKNF_GPU_API int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *ctx,
 		const struct xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
 		const struct xsknf_csum_opts *opts, int32_t *verdicts);
+XSKNF_GPU_API int xsknf_gpu_ctx_submit(struct xsknf_gpu_ctx *ctx, const struct xsknf_gpu_desc *descs,
+		uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts, int32_t *verdicts,
+		uint64_t *ticket);
+XSKNF_GPU_API int xsknf_gpu_ctx_wait(struct xsknf_gpu_ctx *ctx, uint64_t ticket);
 XSKNF_GPU_API int xsknf_gpu_ctx_get_stats(const struct xsknf_gpu_ctx *ctx, struct xsknf_gpu_ctx_stats *stats);
 XSKNF_GPU_API int xsknf_gpu_ctx_destroy(struct xsknf_gpu_ctx *ctx);
 
@@ -215,7 +229,8 @@ XSKNF_GPU_API int xsknf_gpu_hook_get_stats(const struct xsknf_gpu_hook *hook, ui
 		struct xsknf_gpu_ctx_stats *stats);
 XSKNF_GPU_API int xsknf_gpu_hook_destroy(struct xsknf_gpu_hook *hook);
 
-/* Text of the last HIP error seen by this library on the calling thread. */
+/* Text of the last HIP error seen by this library, on any thread (a copy
+ * private to the calling thread). */
 XSKNF_GPU_API const char *xsknf_gpu_last_error(void);
 
 #ifdef __cplusplus

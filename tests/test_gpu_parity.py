@@ -324,14 +324,19 @@ def test_records_only_mode(dev, shape):
     assert np.array_equal(host, ou)
 
 
+@pytest.mark.parametrize("order", ["rx", "scattered"])
 @pytest.mark.parametrize("path", ["zerocopy", "staged"])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
-def test_host_path_bit_exact(dev, path, layout):
-    """UMEM in (pinned) host memory, descriptors / verdicts in host arrays."""
+def test_host_path_bit_exact(dev, path, layout, order):
+    """UMEM in (pinned) host memory, descriptors / verdicts in host arrays.
+    `scattered`: descriptors in a random order, as the fill ring recycles
+    frames -- every batch spans the whole UMEM (STAGED gathers on the CPU)."""
     from xsknf_amd import HostPath
     b = (frames.aligned_batch(3000, "imix", chunk=2048) if layout == "aligned"
          else frames.unaligned_batch(3000, "imix"))
     frames.inject_edge_cases(b, 0.1)
+    if order == "scattered":
+        b.descs = b.descs[np.random.default_rng(5).permutation(b.n)].copy()
     ou, ov = run_oracle(b, iters=3, action=O.REDIRECT, nif=2, ingress=1)
     cs = Checksummer(ChecksummerOptions(action=O.REDIRECT, csum_iterations=3), num_interfaces=2,
                      frame_len_hint=1500)
@@ -346,6 +351,33 @@ def test_host_path_bit_exact(dev, path, layout):
         st = hp.stats()
     assert st["frames"] == b.n
     assert np.array_equal(v, ov)
+    assert np.array_equal(umem, ou)
+
+
+@pytest.mark.parametrize("path", ["zerocopy", "staged"])
+def test_host_path_two_batches_in_flight(dev, path):
+    """xsknf_gpu_ctx_submit / _wait: batches enqueued back to back (two slots in
+    flight, each submit completing the batch two back), contiguous, 2-D-strided
+    and scattered batches mixed, one larger than a slot piece; every verdict and
+    byte equals the oracle's."""
+    from xsknf_amd import HostPath
+    rng = np.random.default_rng(9)
+    b = frames.aligned_batch(80000, "imix", chunk=2048, seed=9)
+    frames.inject_edge_cases(b, 0.05, seed=10)
+    ou, ov = run_oracle(b, iters=1, action=O.DROP, nif=1)
+    perm = np.arange(b.n)
+    perm[5000:9000] = rng.permutation(perm[5000:9000])          # a scattered stretch
+    descs = b.descs[perm].copy()
+    cuts = [0, 64, 1000, 5000, 9000, 9100, 80000]                # 70900 > one 65536-frame piece
+    cs = Checksummer(ChecksummerOptions(action=O.DROP), frame_len_hint=1500)
+    umem = b.umem.copy()
+    outs = [np.full(hi - lo, 7, dtype=np.int32) for lo, hi in zip(cuts[:-1], cuts[1:])]
+    with HostPath(cs, umem, path=path, max_batch=80000) as hp:
+        tickets = [hp.submit(descs[lo:hi], out) for (lo, hi), out in zip(zip(cuts[:-1], cuts[1:]), outs)]
+        hp.wait(tickets[-1])
+        st = hp.stats()
+    assert st["frames"] == b.n
+    assert np.array_equal(np.concatenate(outs), ov[perm])
     assert np.array_equal(umem, ou)
 
 

@@ -2,9 +2,14 @@
 """End-to-end host-path rate (UMEM in host memory, pinned): the rate an AF_XDP
 worker would see calling the GPU batch hook, PCIe included.
 
-For each path (zerocopy / staged) and rx batch size, time back-to-back
-synchronous xsknf_gpu_ctx_process_batch() calls over a host UMEM of 1500 B (or
---len) frames, and check one batch against the CPU oracle.
+For each path (zerocopy / staged), descriptor order and rx batch size, time
+back-to-back batches over a host UMEM of 1500 B (or --len) frames:
+  sync   xsknf_gpu_ctx_process_batch() per batch (one at a time);
+  async  xsknf_gpu_ctx_submit() per batch, waiting for the batch two back (two in flight).
+Orders: `rx` = frames in UMEM order (aligned chunks: the STAGED path moves them
+with one 2-D copy), `scattered` = a random permutation, as the fill ring hands
+frames back (every batch spans the whole UMEM: the STAGED path gathers).
+--check compares the UMEM with the CPU oracle afterwards.
 
     python tools/e2e_bench.py [--frames 1048576] [--len 1500] [--batches 64,4096,65536,1048576]
 """
@@ -30,6 +35,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--paths", default="zerocopy,staged")
+    ap.add_argument("--orders", default="rx,scattered")
+    ap.add_argument("--modes", default="sync,async")
     a = ap.parse_args()
     b = frames.aligned_batch(a.frames, a.len)
     ref = None
@@ -39,26 +46,40 @@ def main():
         O.c_process_batch(ref.umem, ref.descs)
     cs = Checksummer(frame_len_hint=a.len)
     results = []
+    sizes = [int(x) for x in a.batches.split(",")]
     for path in a.paths.split(","):
         umem = b.umem.copy()
-        with HostPath(cs, umem, path=path, max_batch=max(int(x) for x in a.batches.split(","))) as hp:
-            for bs in [int(x) for x in a.batches.split(",")]:
-                bs = min(bs, a.frames)
-                nb = a.frames // bs
-                v = np.empty(bs, dtype=np.int32)
-                hp.process_batch(b.descs[:bs], verdicts=v)   # warm-up
-                done, t0 = 0, time.perf_counter()
-                while time.perf_counter() - t0 < a.seconds or done == 0:
-                    i = done % nb
-                    hp.process_batch(b.descs[i * bs:(i + 1) * bs], verdicts=v)
-                    done += 1
-                dt = time.perf_counter() - t0
-                fr = done * bs
-                results.append({"path": path, "batch": bs, "calls": done,
-                                "us_per_call": round(dt / done * 1e6, 2),
-                                "mpps": round(fr / dt / 1e6, 3),
-                                "gbs_checksummed": round(fr * a.len / dt / 1e9, 3)})
-                print(json.dumps(results[-1]), flush=True)
+        with HostPath(cs, umem, path=path, max_batch=max(sizes)) as hp:
+            for order in a.orders.split(","):
+                descs = b.descs if order == "rx" else \
+                    b.descs[np.random.default_rng(1).permutation(b.n)].copy()
+                for mode in a.modes.split(","):
+                    for bs in sizes:
+                        bs = min(bs, a.frames)
+                        nb = a.frames // bs
+                        vs = [np.empty(bs, dtype=np.int32) for _ in range(3)]
+                        hp.process_batch(descs[:bs], verdicts=vs[0])   # warm-up
+                        done, t0 = 0, time.perf_counter()
+                        tickets = []
+                        while time.perf_counter() - t0 < a.seconds or done == 0:
+                            i = done % nb
+                            d = descs[i * bs:(i + 1) * bs]
+                            if mode == "sync":
+                                hp.process_batch(d, verdicts=vs[0])
+                            else:
+                                tickets.append(hp.submit(d, vs[done % 3]))
+                                if len(tickets) > 2:
+                                    hp.wait(tickets[-3])
+                            done += 1
+                        if tickets:
+                            hp.wait(tickets[-1])
+                        dt = time.perf_counter() - t0
+                        fr = done * bs
+                        results.append({"path": path, "order": order, "mode": mode, "batch": bs, "calls": done,
+                                        "us_per_batch": round(dt / done * 1e6, 2),
+                                        "mpps": round(fr / dt / 1e6, 3),
+                                        "gbs_checksummed": round(fr * a.len / dt / 1e9, 3)})
+                        print(json.dumps(results[-1]), flush=True)
             st = hp.stats()
         if ref is not None:
             # every frame was processed at least once; processing is idempotent

@@ -24,6 +24,8 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_ctx_create",
     "xsknf_gpu_ctx_register_umem",
     "xsknf_gpu_ctx_process_batch",
+    "xsknf_gpu_ctx_submit",
+    "xsknf_gpu_ctx_wait",
     "xsknf_gpu_ctx_get_stats",
     "xsknf_gpu_ctx_destroy",
     "xsknf_gpu_hook_create",
@@ -121,6 +123,12 @@ def load() -> ctypes.CDLL:
     lib.xsknf_gpu_ctx_process_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                 ctypes.c_uint32, ctypes.POINTER(CsumOpts),
                                                 ctypes.c_void_p]
+    lib.xsknf_gpu_ctx_submit.restype = ctypes.c_int
+    lib.xsknf_gpu_ctx_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.POINTER(CsumOpts), ctypes.c_void_p,
+                                         ctypes.POINTER(ctypes.c_uint64)]
+    lib.xsknf_gpu_ctx_wait.restype = ctypes.c_int
+    lib.xsknf_gpu_ctx_wait.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     lib.xsknf_gpu_ctx_get_stats.restype = ctypes.c_int
     lib.xsknf_gpu_ctx_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(CtxStats)]
     lib.xsknf_gpu_ctx_destroy.restype = ctypes.c_int

@@ -204,6 +204,28 @@ class HostPath:
                    "xsknf_gpu_ctx_process_batch")
         return verdicts
 
+    def submit(self, descs, verdicts, ingress_ifindex: int = 0) -> int:
+        """Enqueue a batch (two in flight per context); returns its ticket.  The
+        verdicts array and the batch's frames belong to the context until
+        wait(ticket)."""
+        if descs.dtype.itemsize != 16 or not descs.flags.c_contiguous:
+            raise ValueError("descs must be a contiguous array of 16-byte xdp_desc")
+        n = int(descs.shape[0])
+        if verdicts.shape[0] < n or not verdicts.flags.c_contiguous:
+            raise ValueError("verdicts must be a contiguous int32 array with >= n entries")
+        opts = self.cs.csum_opts()
+        t = ctypes.c_uint64()
+        _lib.check(self._lib.xsknf_gpu_ctx_submit(self._ctx, descs.ctypes.data, n, ingress_ifindex,
+                                                  ctypes.byref(opts), verdicts.ctypes.data, ctypes.byref(t)),
+                   "xsknf_gpu_ctx_submit")
+        self._pending = getattr(self, "_pending", [])
+        self._pending.append((t.value, descs, verdicts))   # keep the arrays alive until waited for
+        return t.value
+
+    def wait(self, ticket: int) -> None:
+        _lib.check(self._lib.xsknf_gpu_ctx_wait(self._ctx, ticket), "xsknf_gpu_ctx_wait")
+        self._pending = [p for p in getattr(self, "_pending", []) if p[0] > ticket]
+
     def stats(self) -> dict:
         st = _lib.CtxStats()
         _lib.check(self._lib.xsknf_gpu_ctx_get_stats(self._ctx, ctypes.byref(st)), "xsknf_gpu_ctx_get_stats")

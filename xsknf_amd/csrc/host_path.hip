@@ -2,61 +2,101 @@
 //
 // In the reference, an AF_XDP worker (src/xsknf.c:716-742) peeks up to
 // batch_size rx descriptors and calls xsknf_packet_processor() on each frame,
-// in place in the worker's mmap'd UMEM (src/xsknf.c:654-672, :958/:975).  This
-// context is what such a worker holds to run that loop on the GPU instead:
-// host UMEM registered once, then one synchronous call per rx batch with the
+// in place in the worker's mmap'd UMEM (src/xsknf.c:654-672, :958/:975), batch
+// after batch.  This context is what such a worker holds to run that loop on
+// the GPU instead: host UMEM registered once, then batches submitted with the
 // descriptors and verdicts in host arrays.
+//
+// Two batches are in flight per context: each of the two SLOTS has its own HIP
+// stream, pinned descriptor / record arrays and staging buffers, so the copies
+// and kernel of one batch overlap the other's, and the host's share of a batch
+// (copy plan, gather, writing the checks) overlaps the device's share of the
+// other.  xsknf_gpu_ctx_submit() / _wait() expose the pipeline; the
+// synchronous xsknf_gpu_ctx_process_batch() cuts a large batch into pieces of
+// kPiece frames and runs them through the same two slots.
 //
 // ZEROCOPY: the UMEM is pinned and mapped into the device address space; the
 //   kernel reads the frames and writes the check bytes over PCIe, in place.
-//   Checks are written in-line (fused stores): a deferred sector rewrite would
-//   re-read sectors over PCIe.
-// STAGED: the byte span of the batch's frames is copied to a device mirror of
-//   the UMEM (hipMemcpyAsync from pinned memory), summed in HBM with every
-//   check deferred, and only the 4-byte per-frame records come back; the host
-//   then writes each frame's 2 check bytes itself.  Copying the span back
-//   instead would overwrite frames outside the batch that the kernel / NIC may
-//   be filling concurrently (fill-ring frames), so it never does.
+//   Checks are written in-line (2-byte stores: host memory has byte enables).
+// STAGED: only the bytes of the batch's frames cross PCIe, into a device
+//   mirror of the UMEM, by the cheapest of
+//     - up to kMaxDmaRuns DMA copies of merged runs (frames closer than
+//       kMergeGap share a run): a contiguous or nearly contiguous batch;
+//     - one 2-D DMA copy (row = frame, pitch = the constant stride): aligned
+//       chunks in rx order, without the gaps between frames;
+//     - a CPU gather of the frames into a pinned staging buffer, one DMA copy,
+//       and descriptors rebased onto it: a scattered batch (the fill ring hands
+//       frames back in recycled order, so a 64-frame batch can span the whole
+//       UMEM);
+//   summed in HBM with every check deferred, and only the 4-byte per-frame
+//   records come back; the host then writes each frame's 2 check bytes.
+//   Copying frames back would overwrite frames outside the batch that the
+//   kernel / NIC may be filling concurrently (fill-ring frames), so it never
+//   does; the mirror is only read by the kernels, so two batches in flight may
+//   share it (their frames are distinct, and a run's gap bytes are the host's
+//   own bytes).
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <new>
+#include <vector>
 
 #include "../../include/xsknf_gpu.h"
 #include "checksummer_internal.h"
+
+namespace {
+
+constexpr int kSlots = 2;
+constexpr uint32_t kPiece = 65536;          // frames per slot submission of process_batch
+constexpr uint64_t kMergeGap = 256;         // frames closer than this share one DMA run
+constexpr size_t kMaxDmaRuns = 8;           // more runs than this (and no 2-D shape): CPU gather
+constexpr uint64_t kOutOfRange = 1ull << 47;   // an address past any UMEM: dropped untouched
+
+struct Run {
+  uint64_t off, len;
+};
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  xsknf_gpu_desc *descs = nullptr;          // pinned; the kernel reads them mapped
+  xsknf_gpu_desc *descs_mapped = nullptr;
+  int32_t *rec = nullptr;                   // pinned; the kernel writes them mapped
+  int32_t *rec_mapped = nullptr;
+  uint8_t *gather = nullptr;                // pinned staging buffer (STAGED, gather plan)
+  uint8_t *gather_dev = nullptr;
+  uint64_t gather_cap = 0;
+  std::vector<uint64_t> offs;               // frame offsets in the host UMEM (STAGED)
+  std::vector<uint32_t> order;
+  std::vector<Run> runs;
+  // the piece in flight
+  bool busy = false;
+  uint64_t seq = 0;
+  uint32_t n = 0;
+  int32_t *out = nullptr;
+  int32_t fwd = -1;
+};
+
+}  // namespace
 
 struct xsknf_gpu_ctx {
   int device = 0;
   int path = XSKNF_GPU_PATH_ZEROCOPY;
   uint32_t max_batch = 0;
+  uint32_t slot_frames = 0;                 // min(max_batch, kPiece)
   uint32_t hint = 0;
-  hipStream_t stream = nullptr;
   uint8_t *umem_host = nullptr;
   uint64_t umem_size = 0;
-  uint8_t *umem_dev = nullptr;        // mapped host pointer (ZEROCOPY) or device mirror (STAGED)
+  uint8_t *umem_dev = nullptr;              // mapped host pointer (ZEROCOPY) or device mirror (STAGED)
   bool registered = false;
-  xsknf_gpu_desc *descs_dev = nullptr;
-  int32_t *verdicts_dev = nullptr;
-  xsknf_gpu_desc *descs_pinned = nullptr;
-  int32_t *verdicts_pinned = nullptr;
-  xsknf_gpu_desc *descs_mapped = nullptr;   // device views of the pinned arrays (direct mode)
-  int32_t *verdicts_mapped = nullptr;
+  Slot slot[kSlots];
+  int next = 0;                             // slot the next piece goes to (round robin)
+  uint64_t seq = 0;                         // pieces submitted
   xsknf_gpu_ctx_stats stats = {};
 };
-
-// Direct mode (the default): the kernel reads the descriptors from, and
-// writes the verdicts / records to, the pinned host arrays themselves, so a
-// call is one launch and one synchronize -- no H2D descriptor copy and no D2H
-// verdict copy, each a separate DMA command with its own latency (a batch of 64
-// frames: 39 us per call with both copies).  -DXSKNF_CTX_COPY_ARRAYS keeps the
-// copies (A/B builds).
-#ifdef XSKNF_CTX_COPY_ARRAYS
-constexpr bool kDirect = false;
-#else
-constexpr bool kDirect = true;
-#endif
 
 namespace {
 
@@ -72,15 +112,225 @@ uint64_t umem_offset(uint64_t addr) {
 void release(xsknf_gpu_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (Slot &s : c->slot) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.descs) (void)hipHostFree(s.descs);
+    if (s.rec) (void)hipHostFree(s.rec);
+    if (s.gather) (void)hipHostFree(s.gather);
+    if (s.gather_dev) (void)hipFree(s.gather_dev);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
   if (c->registered) (void)hipHostUnregister(c->umem_host);
   if (c->path == XSKNF_GPU_PATH_STAGED && c->umem_dev) (void)hipFree(c->umem_dev);
-  if (c->descs_dev) (void)hipFree(c->descs_dev);
-  if (c->verdicts_dev) (void)hipFree(c->verdicts_dev);
-  if (c->descs_pinned) (void)hipHostFree(c->descs_pinned);
-  if (c->verdicts_pinned) (void)hipHostFree(c->verdicts_pinned);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+// Finish the slot's piece: wait for its stream, then (STAGED) write the checks
+// into the host UMEM from the records, and hand out the verdicts.
+int complete(xsknf_gpu_ctx *c, Slot &s) {
+  using namespace xsknf_gpu;
+  if (!s.busy) return 0;
+  s.busy = false;
+  hipError_t e = hipEventSynchronize(s.done);
+  if (e != hipSuccess) return fail(e, "hipEventSynchronize");
+  if (c->path == XSKNF_GPU_PATH_STAGED) {
+    // checksummer_user.c:108 on the host: the 2 check bytes of every summed frame
+    for (uint32_t i = 0; i < s.n; ++i) {
+      const uint32_t r = static_cast<uint32_t>(s.rec[i]);
+      if ((r & kRecTagMask) == kRecTag) {
+        uint8_t *p = c->umem_host + s.offs[i] + ((r >> 16) & 0x7f) + 6;
+        p[0] = static_cast<uint8_t>(r);
+        p[1] = static_cast<uint8_t>(r >> 8);
+        s.out[i] = s.fwd;
+      } else {
+        s.out[i] = static_cast<int32_t>(r);
+      }
+    }
+  } else {
+    memcpy(s.out, s.rec, sizeof(int32_t) * s.n);
+  }
+  c->stats.batches += 1;
+  c->stats.frames += s.n;
+  c->stats.bytes_d2h += sizeof(int32_t) * s.n;
+  return 0;
+}
+
+// Complete every piece with a sequence number <= upto, oldest first.
+int complete_upto(xsknf_gpu_ctx *c, uint64_t upto) {
+  for (;;) {
+    Slot *old = nullptr;
+    for (Slot &s : c->slot)
+      if (s.busy && s.seq <= upto && (!old || s.seq < old->seq)) old = &s;
+    if (!old) return 0;
+    const int rc = complete(c, *old);
+    if (rc) return rc;
+  }
+}
+
+int grow_gather(xsknf_gpu_ctx *c, Slot &s, uint64_t need) {
+  if (need <= s.gather_cap) return 0;
+  uint64_t cap = s.gather_cap ? s.gather_cap : (1u << 20);
+  while (cap < need) cap *= 2;
+  if (s.gather) (void)hipHostFree(s.gather);
+  if (s.gather_dev) (void)hipFree(s.gather_dev);
+  s.gather = nullptr;
+  s.gather_dev = nullptr;
+  s.gather_cap = 0;
+  hipError_t e = hipHostMalloc(&s.gather, cap, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc(&s.gather_dev, cap + 16);   // + the last chunk's 16-byte read
+  if (e != hipSuccess) return fail(e, "staging buffer");
+  s.gather_cap = cap;
+  (void)c;
+  return 0;
+}
+
+// STAGED: move the piece's frame bytes to the device and point the kernel at
+// them.  Sets umem / umem_size of `a` (the mirror, or the slot's staging
+// buffer with the slot's descriptors rebased onto it).
+int stage_frames(xsknf_gpu_ctx *c, Slot &s, uint32_t n, xsknf_gpu::KernelArgs &a) {
+  s.offs.resize(n);
+  s.order.clear();
+  bool sorted = true;
+  uint64_t prev = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t off = umem_offset(s.descs[i].addr);
+    const uint32_t len = s.descs[i].len;
+    s.offs[i] = off;
+    if (off > c->umem_size || len > c->umem_size - off || len == 0) continue;
+    if (off < prev) sorted = false;
+    prev = off;
+    s.order.push_back(i);
+  }
+  if (!sorted)
+    std::sort(s.order.begin(), s.order.end(), [&](uint32_t x, uint32_t y) { return s.offs[x] < s.offs[y]; });
+  // merged runs
+  s.runs.clear();
+  for (uint32_t i : s.order) {
+    const uint64_t off = s.offs[i], end = off + s.descs[i].len;
+    if (!s.runs.empty() && off <= s.runs.back().off + s.runs.back().len + kMergeGap) {
+      Run &r = s.runs.back();
+      if (end > r.off + r.len) r.len = end - r.off;
+    } else {
+      s.runs.push_back(Run{off, end - off});
+    }
+  }
+  a.umem = c->umem_dev;
+  a.umem_size = c->umem_size;
+  uint64_t moved = 0;
+  hipError_t e = hipSuccess;
+  if (s.runs.size() <= kMaxDmaRuns) {
+    for (const Run &r : s.runs) {
+      e = hipMemcpyAsync(c->umem_dev + r.off, c->umem_host + r.off, r.len, hipMemcpyHostToDevice, s.stream);
+      if (e != hipSuccess) return fail(e, "hipMemcpyAsync(run)");
+      moved += r.len;
+    }
+  } else {
+    // one 2-D copy when the frames sit at a constant stride (aligned chunks in rx order)
+    const size_t k = s.order.size();
+    const uint64_t o0 = s.offs[s.order[0]];
+    const uint64_t stride = s.offs[s.order[1]] - o0;
+    uint32_t width = 0;
+    bool uniform = stride > 0;
+    for (size_t j = 0; uniform && j < k; ++j) {
+      uniform = s.offs[s.order[j]] == o0 + j * stride;
+      width = std::max(width, s.descs[s.order[j]].len);
+    }
+    uniform = uniform && width <= stride && o0 + (k - 1) * stride + width <= c->umem_size;
+    if (uniform) {
+      e = hipMemcpy2DAsync(c->umem_dev + o0, stride, c->umem_host + o0, stride, width, k, hipMemcpyHostToDevice,
+                           s.stream);
+      if (e != hipSuccess) return fail(e, "hipMemcpy2DAsync(frames)");
+      moved = static_cast<uint64_t>(width) * k;
+    } else {
+      // CPU gather into the pinned staging buffer (each frame keeps its 16-byte
+      // phase), one DMA copy, descriptors rebased onto the staging buffer
+      uint64_t need = 0;
+      for (uint32_t i : s.order) need = ((need + 15) & ~15ull) + 16 + s.descs[i].len;
+      int rc = grow_gather(c, s, need);
+      if (rc) return rc;
+      std::vector<uint64_t> &pos = s.offs;   // keep the host offsets: rebased copies go to descs
+      uint64_t at = 0;
+      for (uint32_t i = 0; i < n; ++i) s.descs[i].addr = kOutOfRange;
+      for (uint32_t i : s.order) {
+        at = ((at + 15) & ~15ull) + (pos[i] & 15);
+        memcpy(s.gather + at, c->umem_host + pos[i], s.descs[i].len);
+        s.descs[i].addr = at;
+        at += s.descs[i].len;
+      }
+      e = hipMemcpyAsync(s.gather_dev, s.gather, at, hipMemcpyHostToDevice, s.stream);
+      if (e != hipSuccess) return fail(e, "hipMemcpyAsync(gather)");
+      a.umem = s.gather_dev;
+      a.umem_size = at;
+      moved = at;
+    }
+  }
+  c->stats.bytes_h2d += moved;
+  return 0;
+}
+
+// Enqueue one piece (n <= slot_frames) into the next slot.
+int submit_piece(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
+                 const xsknf_csum_opts *opts, int32_t *verdicts) {
+  using namespace xsknf_gpu;
+  Slot &s = c->slot[c->next];
+  int rc = complete(c, s);
+  if (rc) return rc;
+  KernelArgs a;
+  rc = prepare(a, c->umem_dev, c->umem_size, s.descs_mapped, n, ingress_ifindex, opts, s.rec_mapped);
+  if (rc != 0) return rc < 0 ? rc : 0;
+  memcpy(s.descs, descs, sizeof(xsknf_gpu_desc) * n);
+  c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
+
+  xsknf_gpu_launch_cfg cfg;
+  default_cfg(c->hint ? c->hint : 2048u, cfg);
+  if (c->path == XSKNF_GPU_PATH_STAGED) {
+    rc = stage_frames(c, s, n, a);
+    if (rc) return rc;
+    cfg.fused_stores = 3;   // records only: the checks are applied on the host (complete())
+  } else {
+    if (n <= 2048) {
+      // A small batch is a few 64-frame tiles: the split kernel would read it
+      // over PCIe with a few waves.  The group kernel spreads it over many
+      // (4 or 2 frames per wave), so more reads are in flight
+      // (tools/small_batch.py, 1500 B: 64 frames 44.8 -> 18.8 us per call,
+      // 256: 46.8 -> 24.1, 1024: 51.0 -> 45.0; equal from 4096).
+      cfg.kernel = XSKNF_GPU_KERNEL_AUTO;
+      cfg.window_chunks = 0;
+      cfg.lds_ring = 0;
+      cfg.lanes_per_frame = n <= 256 ? 32 : 64;
+      cfg.chunks_per_lane = n <= 256 ? 3 : 2;
+      cfg.frames_per_group = n <= 256 ? 2 : 4;
+    }
+    cfg.fused_stores = 1;   // in place over PCIe, ...
+    a.sector_stores = 0;    // ... as 2-byte writes (byte enables; no RMW in host memory)
+  }
+  rc = run(a, cfg, s.stream);
+  if (rc != 0) return rc;
+  hipError_t e = hipEventRecord(s.done, s.stream);
+  if (e != hipSuccess) return fail(e, "hipEventRecord");
+  s.busy = true;
+  s.seq = ++c->seq;
+  s.n = n;
+  s.out = verdicts;
+  s.fwd = a.fwd_verdict;
+  c->next = (c->next + 1) % kSlots;
+  return 0;
+}
+
+int submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
+           const xsknf_csum_opts *opts, int32_t *verdicts, uint64_t *ticket) {
+  if (!c || !c->registered || n > c->max_batch) return -EINVAL;
+  if (n && (!descs || !verdicts)) return -EINVAL;
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return fail(e, "hipSetDevice");
+  for (uint32_t p = 0; p < n; p += c->slot_frames) {
+    const uint32_t k = std::min(c->slot_frames, n - p);
+    const int rc = submit_piece(c, descs + p, k, ingress_ifindex, opts, verdicts + p);
+    if (rc) return rc;
+  }
+  if (ticket) *ticket = c->seq;
+  return 0;
 }
 
 }  // namespace
@@ -97,15 +347,17 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
   c->device = device;
   c->path = path;
   c->max_batch = max_batch;
+  c->slot_frames = std::min(max_batch, kPiece);
   c->hint = frame_len_hint;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipMalloc(&c->descs_dev, sizeof(xsknf_gpu_desc) * max_batch);
-  if (e == hipSuccess) e = hipMalloc(&c->verdicts_dev, sizeof(int32_t) * max_batch);
-  if (e == hipSuccess) e = hipHostMalloc(&c->descs_pinned, sizeof(xsknf_gpu_desc) * max_batch, hipHostMallocDefault);
-  if (e == hipSuccess) e = hipHostMalloc(&c->verdicts_pinned, sizeof(int32_t) * max_batch, hipHostMallocDefault);
-  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->descs_mapped), c->descs_pinned, 0);
-  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->verdicts_mapped), c->verdicts_pinned, 0);
+  for (Slot &s : c->slot) {
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc(&s.descs, sizeof(xsknf_gpu_desc) * c->slot_frames, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc(&s.rec, sizeof(int32_t) * c->slot_frames, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.descs_mapped), s.descs, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.rec_mapped), s.rec, 0);
+  }
   if (e != hipSuccess) {
     const int rc = fail(e, "xsknf_gpu_ctx_create");
     release(c);
@@ -129,7 +381,7 @@ int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *c, void *umem, uint64_t si
     e = hipHostGetDevicePointer(&dp, umem, 0);
     c->umem_dev = static_cast<uint8_t *>(dp);
   } else {
-    e = hipMalloc(&c->umem_dev, size);
+    e = hipMalloc(&c->umem_dev, size + 16);   // + the last chunk's 16-byte read
   }
   if (e != hipSuccess) {
     (void)hipHostUnregister(umem);
@@ -140,90 +392,30 @@ int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *c, void *umem, uint64_t si
   return 0;
 }
 
+int xsknf_gpu_ctx_submit(struct xsknf_gpu_ctx *c, const struct xsknf_gpu_desc *descs, uint32_t n,
+                         uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts, int32_t *verdicts,
+                         uint64_t *ticket) {
+  if (!ticket) return -EINVAL;
+  return submit(c, descs, n, ingress_ifindex, opts, verdicts, ticket);
+}
+
+int xsknf_gpu_ctx_wait(struct xsknf_gpu_ctx *c, uint64_t ticket) {
+  if (!c) return -EINVAL;
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return fail(e, "hipSetDevice");
+  return complete_upto(c, ticket);
+}
+
 int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *c, const struct xsknf_gpu_desc *descs, uint32_t n,
                                 uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
                                 int32_t *verdicts) {
-  using namespace xsknf_gpu;
-  if (!c || !c->registered || n > c->max_batch) return -EINVAL;
-  if (n == 0) return 0;
-  if (!descs || !verdicts) return -EINVAL;
-  KernelArgs a;
-  int rc = prepare(a, c->umem_dev, c->umem_size, kDirect ? c->descs_mapped : c->descs_dev, n, ingress_ifindex,
-                   opts, kDirect ? c->verdicts_mapped : c->verdicts_dev);
-  if (rc != 0) return rc < 0 ? rc : 0;
-  hipError_t e = hipSetDevice(c->device);
-  if (e != hipSuccess) return fail(e, "hipSetDevice");
-
-  memcpy(c->descs_pinned, descs, sizeof(xsknf_gpu_desc) * n);
-  if (!kDirect) {
-    e = hipMemcpyAsync(c->descs_dev, c->descs_pinned, sizeof(xsknf_gpu_desc) * n, hipMemcpyHostToDevice,
-                       c->stream);
-    if (e != hipSuccess) return fail(e, "hipMemcpyAsync(descs)");
+  uint64_t t = 0;
+  const int rc = submit(c, descs, n, ingress_ifindex, opts, verdicts, &t);
+  if (rc) {
+    if (c) (void)complete_upto(c, UINT64_MAX);   // leave nothing in flight
+    return rc;
   }
-  c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
-
-  xsknf_gpu_launch_cfg cfg;
-  default_cfg(c->hint ? c->hint : 2048u, cfg);
-  if (c->path == XSKNF_GPU_PATH_ZEROCOPY && n <= 2048) {
-    // A small batch is a few 64-frame tiles: the split kernel would read it
-    // over PCIe with a few waves.  The group kernel spreads it over many
-    // (4 or 2 frames per wave), so more reads are in flight
-    // (tools/small_batch.py, 1500 B: 64 frames 44.8 -> 18.8 us per call,
-    // 256: 46.8 -> 24.1, 1024: 51.0 -> 45.0; equal from 4096).
-    cfg.kernel = XSKNF_GPU_KERNEL_AUTO;
-    cfg.window_chunks = 0;
-    cfg.lds_ring = 0;
-    cfg.lanes_per_frame = n <= 256 ? 32 : 64;
-    cfg.chunks_per_lane = n <= 256 ? 3 : 2;
-    cfg.frames_per_group = n <= 256 ? 2 : 4;
-  }
-  if (c->path == XSKNF_GPU_PATH_STAGED) {
-    // byte span of the batch's (in-range) frames
-    uint64_t lo = UINT64_MAX, hi = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint64_t off = umem_offset(descs[i].addr);
-      if (off > c->umem_size || descs[i].len > c->umem_size - off) continue;
-      lo = off < lo ? off : lo;
-      hi = off + descs[i].len > hi ? off + descs[i].len : hi;
-    }
-    if (hi > lo) {
-      e = hipMemcpyAsync(c->umem_dev + lo, c->umem_host + lo, hi - lo, hipMemcpyHostToDevice, c->stream);
-      if (e != hipSuccess) return fail(e, "hipMemcpyAsync(umem span)");
-      c->stats.bytes_h2d += hi - lo;
-    }
-    cfg.fused_stores = 3;   // records only: the checks are applied on the host below
-  } else {
-    cfg.fused_stores = 1;   // in place over PCIe, ...
-    a.sector_stores = 0;    // ... as 2-byte writes (byte enables; no RMW in host memory)
-  }
-  rc = run(a, cfg, c->stream);
-  if (rc != 0) return rc;
-  e = kDirect ? hipSuccess
-              : hipMemcpyAsync(c->verdicts_pinned, c->verdicts_dev, sizeof(int32_t) * n, hipMemcpyDeviceToHost,
-                               c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  if (e != hipSuccess) return fail(e, "verdict copy-back");
-  c->stats.bytes_d2h += sizeof(int32_t) * n;
-
-  if (c->path == XSKNF_GPU_PATH_STAGED) {
-    // checksummer_user.c:108 on the host: the 2 check bytes of every summed frame
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t r = static_cast<uint32_t>(c->verdicts_pinned[i]);
-      if ((r & kRecTagMask) == kRecTag) {
-        uint8_t *p = c->umem_host + umem_offset(descs[i].addr) + ((r >> 16) & 0x7f) + 6;
-        p[0] = static_cast<uint8_t>(r);
-        p[1] = static_cast<uint8_t>(r >> 8);
-        verdicts[i] = a.fwd_verdict;
-      } else {
-        verdicts[i] = static_cast<int32_t>(r);
-      }
-    }
-  } else {
-    memcpy(verdicts, c->verdicts_pinned, sizeof(int32_t) * n);
-  }
-  c->stats.batches += 1;
-  c->stats.frames += n;
-  return 0;
+  return complete_upto(c, t);
 }
 
 int xsknf_gpu_ctx_get_stats(const struct xsknf_gpu_ctx *c, struct xsknf_gpu_ctx_stats *stats) {
@@ -234,6 +426,8 @@ int xsknf_gpu_ctx_get_stats(const struct xsknf_gpu_ctx *c, struct xsknf_gpu_ctx_
 
 int xsknf_gpu_ctx_destroy(struct xsknf_gpu_ctx *c) {
   if (!c) return -EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)complete_upto(c, UINT64_MAX);
   release(c);
   return 0;
 }
@@ -350,7 +544,7 @@ int xsknf_gpu_hook_destroy(struct xsknf_gpu_hook *h) {
   if (!h) return -EINVAL;
   for (uint32_t i = 0; i < h->workers; ++i)
     for (HookSlot &s : h->w[i].slot)
-      if (s.ctx) release(s.ctx);
+      if (s.ctx) xsknf_gpu_ctx_destroy(s.ctx);
   delete[] h->w;
   delete h;
   return 0;
