@@ -181,8 +181,8 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     n = int(lens_in.shape[0])
     umem, descs, lens = frames.device_batch(n, lens_in, layout=layout, chunk=chunk or frames.CHUNK, seed=seed,
                                             device=dev)
-    hint = int(lens.max())
-    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint)
+    hint, mean = int(lens.max()), int(lens.mean())      # what the caller knows of its batch
+    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint, frame_len_mean=mean)
     verdicts = torch.empty(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     umem_ptr, descs_ptr, v_ptr = umem.data_ptr(), descs.data_ptr(), verdicts.data_ptr()
@@ -233,7 +233,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     from xsknf_amd import _lib
     lib = _lib.load()
     cfg = _lib.LaunchCfg()
-    _lib.check(lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(cfg)), "default_launch_cfg")
+    _lib.check(lib.xsknf_gpu_launch_cfg_for_lens(hint, mean, ctypes.byref(cfg)), "launch_cfg_for_lens")
     single_kernel = (cfg.fused_stores & 3) == 1
     family = "checksum_kernel_split" if cfg.kernel == 1 else "checksum_kernel"
     k_ms = None

@@ -44,6 +44,7 @@
 #include <stdint.h>
 #include <errno.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/xsknf_gpu.h"
@@ -1495,7 +1496,12 @@ int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && a.defer_min_len != kNoDefer && !a.no_scatter && !a.tail_scatter) {
     const uint32_t need = (4 * a.n + kBlock - 1) / kBlock;   // dense shape: 4 lanes per frame
-    const uint32_t cap = static_cast<uint32_t>(device_cus() * 8);
+    int bpc = 8;   // scatter blocks per CU
+#ifdef XSKNF_AB
+    static const int ab_bpc = getenv("XSKNF_SCATTER_BPC") ? atoi(getenv("XSKNF_SCATTER_BPC")) : 8;
+    bpc = ab_bpc > 0 ? ab_bpc : 8;
+#endif
+    const uint32_t cap = static_cast<uint32_t>(device_cus() * bpc);
     hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
     e = hipGetLastError();
     what = "scatter_checks launch";
@@ -1593,8 +1599,9 @@ const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   return nullptr;
 }
 
-// Default shape for a length hint.
-void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
+// Default shape for a batch whose longest frame is `hint` bytes and whose mean
+// length is `mean` (0 = unknown).
+void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   c.frames_per_group = 4;
   c.blocks_per_cu = 8;
   c.lds_ring = 0;
@@ -1615,7 +1622,10 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.lanes_per_frame = 16;
   if (hint <= 128) {
     c.window_chunks = 4 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1 + 8;
-  } else if (hint < kDeferMinLen) {
+  } else if (hint < kDeferMinLen || (mean && mean < kDeferMinLen)) {
+    // also a mix of mostly short frames (IMIX, mean 352 B): its tiles almost
+    // never defer, so every check in-line and no scatter launch (IMIX 1M
+    // frames: 105 -> 100 us)
     c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1 + 8;
   } else if (hint + 15 <= 4096) {
     c.window_chunks = 8 + 16; c.chunks_per_lane = 3; c.frames_per_group = 1; c.fused_stores = 0;
@@ -1711,6 +1721,25 @@ int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct
 int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg) {
   if (!cfg) return -EINVAL;
   xsknf_gpu::default_cfg(frame_len_hint ? frame_len_hint : 2048u, *cfg);
+  return 0;
+}
+
+int xsknf_gpu_checksum_batch_lens(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
+                                  uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+                                  int32_t *verdicts, uint32_t frame_len_max, uint32_t frame_len_mean,
+                                  void *stream) {
+  xsknf_gpu::KernelArgs a;
+  const int rc = xsknf_gpu::prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
+  if (rc != 0) return rc < 0 ? rc : 0;
+  xsknf_gpu_launch_cfg cfg;
+  xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, cfg, frame_len_mean);
+  return xsknf_gpu::run(a, cfg, stream);
+}
+
+int xsknf_gpu_launch_cfg_for_lens(uint32_t frame_len_max, uint32_t frame_len_mean,
+                                  struct xsknf_gpu_launch_cfg *cfg) {
+  if (!cfg) return -EINVAL;
+  xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, *cfg, frame_len_mean);
   return 0;
 }
 
