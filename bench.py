@@ -78,6 +78,9 @@ def parse():
     p.add_argument("--root-scatter", action="store_true",
                    help="N > 1: also time the distribution of a root-resident global IMIX batch "
                         "(SURVEY 8(e) collective 1), reported as `root_scatter`")
+    p.add_argument("--rotate", type=int, default=0,
+                   help="batches the steps cycle through (0 = enough to exceed --rotate-bytes)")
+    p.add_argument("--rotate-bytes", type=int, default=1 << 30)
     p.add_argument("--kernel-steps", type=int, default=50,
                    help="launches of the summing kernel alone (records only), reported beside the step")
     return p.parse_args()
@@ -175,17 +178,35 @@ def workload_lengths(name, args, world, rank):
     return frames._lens(args.frames, length, np.random.default_rng(frames.SEED + rank)), None
 
 
+def rotation(lens: np.ndarray, args) -> int:
+    """Batches the steps cycle through: enough that what one pass touches (the
+    frames' 64-B sectors, descriptors, verdicts) times K exceeds --rotate-bytes,
+    so a step never finds the previous pass's bytes in the 256 MiB Infinity
+    Cache -- a 1M-frame 64 B batch touches 84 MB, and re-reading it step after
+    step would be served partly on-die.  A 1500 B batch (1.6 GB) needs K = 1."""
+    if args.rotate > 0:
+        return args.rotate
+    touched = int(((lens.astype(np.int64) + 63) // 64 * 64).sum()) + 20 * lens.shape[0]
+    return int(min(16, max(1, -(-args.rotate_bytes // max(1, touched)))))
+
+
 def time_workload(name, args, world, rank, dev, seed, primary):
     length, layout, chunk, desc = WORKLOADS[name]
     lens_in, span = workload_lengths(name, args, world, rank)
     n = int(lens_in.shape[0])
-    umem, descs, lens = frames.device_batch(n, lens_in, layout=layout, chunk=chunk or frames.CHUNK, seed=seed,
-                                            device=dev)
+    K = rotation(lens_in, args)
+    # K batches of the same shape in one UMEM (batch j = frames [j*n, (j+1)*n)),
+    # step i processes batch i % K
+    umem, descs, lens = frames.device_batch(n * K, np.tile(lens_in, K), layout=layout, chunk=chunk or frames.CHUNK,
+                                            seed=seed, device=dev)
     hint, mean = int(lens.max()), int(lens.mean())      # what the caller knows of its batch
     cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint, frame_len_mean=mean)
-    verdicts = torch.empty(n, dtype=torch.int32, device=dev)
+    verdicts = torch.empty(n * K, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
-    umem_ptr, descs_ptr, v_ptr = umem.data_ptr(), descs.data_ptr(), verdicts.data_ptr()
+    umem_ptr, umem_size = umem.data_ptr(), umem.numel()
+    descs_ptrs = [descs.data_ptr() + 16 * n * j for j in range(K)]
+    v_ptrs = [verdicts.data_ptr() + 4 * n * j for j in range(K)]
+    batch_bytes = [int(lens[j * n:(j + 1) * n].sum()) for j in range(K)]
 
     # a bounded host sample of the ORIGINAL frames for the CPU baseline leg
     sample = None
@@ -196,8 +217,12 @@ def time_workload(name, args, world, rank, dev, seed, primary):
         hi = int((offs + dk["len"]).max())
         sample = (umem[:hi].cpu().numpy(), dk, k)
 
+    it = [0]
+
     def step():
-        cs.process_batch_ptr(umem_ptr, umem.numel(), descs_ptr, n, v_ptr, 0, stream.cuda_stream)
+        j = it[0] % K
+        it[0] += 1
+        cs.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[j], n, v_ptrs[j], 0, stream.cuda_stream)
 
     # W untimed warmup steps, continued until at least --min-warmup-s of
     # warmup has run: measured on MI355X, 10 steps (3 ms) leave the step ~3 %
@@ -214,12 +239,15 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    first = it[0]
     ev0.record(stream)
     for _ in range(args.steps):
         step()
     ev1.record(stream)
     barrier(world)
     wall = time.perf_counter() - t0
+    # frame bytes of the timed steps (the K batches differ slightly in length mix)
+    bytes_len = sum(batch_bytes[i % K] for i in range(first, first + args.steps)) // args.steps
     step_ms = ev0.elapsed_time(ev1) / args.steps        # HIP events on the launch stream
     wall_max = allreduce_max(wall, world)
     step_ms_max = allreduce_max(step_ms, world)
@@ -242,9 +270,13 @@ def time_workload(name, args, world, rank, dev, seed, primary):
         rec = torch.empty(n, dtype=torch.int32, device=dev)
         opts = cs.csum_opts()
 
+        kit = [0]
+
         def kstep():
+            j = kit[0] % K
+            kit[0] += 1
             rc = lib.xsknf_gpu_checksum_batch_cfg(
-                ctypes.c_void_p(umem_ptr), umem.numel(), ctypes.c_void_p(descs_ptr), n, 0, ctypes.byref(opts),
+                ctypes.c_void_p(umem_ptr), umem_size, ctypes.c_void_p(descs_ptrs[j]), n, 0, ctypes.byref(opts),
                 ctypes.c_void_p(rec.data_ptr()), ctypes.byref(cfg), ctypes.c_void_p(stream.cuda_stream))
             _lib.check(rc, "records-only launch")
 
@@ -261,10 +293,10 @@ def time_workload(name, args, world, rank, dev, seed, primary):
         k_ms = e0.elapsed_time(e1) / args.kernel_steps
         del rec
 
-    vh = verdicts.cpu().numpy()
-    bytes_len = int(lens.sum())
+    vh = verdicts[:n].cpu().numpy()
     counters = allreduce_sum_i64([n, bytes_len, int((vh == -1).sum()), int((vh >= 0).sum())], world)
-    return dict(name=name, desc=desc, n=n, lens=lens, bytes_len=bytes_len, step_ms=step_ms, step_ms_max=step_ms_max,
+    return dict(name=name, desc=desc, n=n, K=K, lens=lens, bytes_len=bytes_len, step_ms=step_ms,
+                step_ms_max=step_ms_max,
                 sum_ms=k_ms, single_kernel=single_kernel, family=family, wall_max=wall_max, counters=counters,
                 umem=umem, descs=descs, verdicts=verdicts, sample=sample, layout=layout, chunk=chunk, span=span)
 
@@ -379,7 +411,7 @@ def attainable_for(res, reps=20):
     if not os.path.exists(path):
         return None
     lens = res["lens"]
-    n = res["n"]
+    n = res["n"] * res["K"]          # every rotated batch: the probe reads cold bytes too
     if res["layout"] == "aligned":
         if int(lens.min()) != int(lens.max()):
             return None
@@ -400,6 +432,8 @@ def attainable_for(res, reps=20):
     if us <= 0:
         return None
     gbs = probe_bytes / us / 1e3
+    us /= res["K"]                    # per batch
+    probe_bytes //= res["K"]
     out = {"read_GBps": round(gbs, 1), "probe_us": round(us, 2), "probe_bytes": probe_bytes,
            "probe": "tools/hbm_probe.hip: fastest of its read shapes over the same bytes, nothing written"}
     k_ms = res["sum_ms"] if res["sum_ms"] is not None else (res["step_ms"] if res["single_kernel"] else None)
@@ -430,7 +464,7 @@ def step_summary(r, steps):
     out = {"frames": total_frames, "mpps": round(total_frames / t / 1e6, 2),
            "gbs_checksummed": round(total_bytes / t / 1e9, 2), "step_us": round(r["step_ms_max"] * 1e3, 2),
            "step_frac": round(alg / t / 1e9 / HBM_PEAK_GBS / max(1, r.get("world", 1)), 4),
-           "wall_ms_per_step": round(r["wall_max"] / steps * 1e3, 4)}
+           "wall_ms_per_step": round(r["wall_max"] / steps * 1e3, 4), "rotated_batches": r["K"]}
     if r["span"] is not None:
         out["rank0_shard"] = list(r["span"])
     return out
@@ -498,7 +532,7 @@ def main():
             "vs_baseline": None, "dtype": "u16 words summed in u32", "data": "synthetic",
             "mpps": round(mpps, 2),
             "config": {"workload": desc, "frames_per_gpu": prim["n"], "frame_len": length,
-                       "layout": layout, "global_batch": total_frames,
+                       "layout": layout, "global_batch": total_frames, "rotated_batches": prim["K"],
                        "parallelism": f"shard{world} (independent frames, no exchange)"},
             "roofline": roof, "cpu_baseline": cpu, "secondary": sec,
             "verdicts": {"drop": n_drop, "forward": n_fwd},

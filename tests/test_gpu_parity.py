@@ -226,6 +226,8 @@ PRODUCT_SHAPES = [
     (16, 3, 1, 0, 0, 1, 24), (16, 3, 1, 0, 1, 1, 24), (16, 3, 1, 0, 2, 1, 24), (16, 3, 1, 0, 16, 1, 24),
     (16, 3, 1, 0, 18, 1, 24), (16, 3, 1, 0, 4, 1, 24),
     (16, 3, 2, 0, 0, 1, 20), (16, 3, 2, 0, 2, 1, 20), (16, 3, 2, 0, 20, 1, 20), (16, 3, 2, 0, 1, 1, 20),
+    # the lane kernel (short frames) under every store mode
+    (1, 5, 2, 0, 1), (1, 5, 2, 0, 9), (1, 5, 2, 0, 5), (1, 5, 2, 0, 2), (1, 5, 2, 0, 0),
     # the zero-copy host path's small-batch group shapes
     (32, 3, 2, 0, 0), (32, 3, 2, 0, 1), (32, 3, 2, 0, 5), (64, 2, 4, 0, 2), (64, 2, 4, 0, 1),
 ]
@@ -235,7 +237,7 @@ AB_SHAPES = [
     (64, 9, 2, 0, 2), (64, 2, 8, 0, 0), (8, 1, 1, 3, 2), (16, 2, 1, 3, 1), (32, 3, 1, 2, 0), (32, 3, 1, 3, 1),
     (64, 4, 1, 3, 0), (64, 2, 1, 4, 1),
     (4, 2, 4, 0, 1), (4, 2, 2, 0, 0), (4, 2, 4, 0, 5),
-    (1, 5, 2, 0, 1), (1, 5, 4, 0, 0), (1, 6, 2, 0, 9), (1, 7, 2, 0, 5), (1, 5, 2, 0, 2),
+    (1, 5, 4, 0, 0), (1, 6, 2, 0, 9), (1, 7, 2, 0, 5),
     (8, 1, 4, 0, 5), (16, 2, 4, 0, 4), (32, 3, 4, 0, 5),
     (16, 2, 2, 0, 0, 1, 4), (16, 2, 1, 0, 1, 1, 4), (8, 4, 2, 0, 2, 1, 4), (32, 1, 2, 0, 5, 1, 4),
     (16, 4, 1, 0, 4, 1, 4), (16, 2, 2, 0, 0, 1, 5), (64, 2, 1, 0, 0, 1, 4), (32, 2, 1, 0, 1, 1, 4),

@@ -40,10 +40,18 @@ def main():
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="batches the timed launches cycle through (bench.py's rotation: keeps a small-frame "
+                         "batch out of the Infinity Cache between launches)")
     a = ap.parse_args()
     length, layout = WL[a.workload]
     dev = torch.device("cuda:0")
-    umem0, descs, lens = frames.device_batch(a.frames, length, layout=layout, device=dev)
+    K = max(1, a.rotate)
+    base_lens = frames._lens(a.frames, length, __import__("numpy").random.default_rng(frames.SEED))
+    umem0, descs_all, lens_all = frames.device_batch(a.frames * K, __import__("numpy").tile(base_lens, K),
+                                                     layout=layout, device=dev)
+    descs = descs_all[:a.frames]
+    lens = lens_all[:a.frames]
     lib = _lib.load()
     opts = _lib.CsumOpts(1, 0, 1, 0)
     n = a.frames
@@ -63,10 +71,12 @@ def main():
     umem = umem0.clone()
     verd = torch.empty(n, dtype=torch.int32, device=dev)
 
-    def run(cfg, um, vv):
+    rot = [0]
+
+    def run(cfg, um, vv, j=0):
         c = _lib.LaunchCfg(cfg[0][0], cfg[0][1], cfg[0][2], cfg[1], cfg[0][3], cfg[0][4], cfg[0][5], cfg[0][6])
         rc = lib.xsknf_gpu_checksum_batch_cfg(ctypes.c_void_p(um.data_ptr()), um.numel(),
-                                              ctypes.c_void_p(descs.data_ptr()), n, 0,
+                                              ctypes.c_void_p(descs_all.data_ptr() + 16 * n * j), n, 0,
                                               ctypes.byref(opts), ctypes.c_void_p(vv.data_ptr()),
                                               ctypes.byref(c), ctypes.c_void_p(stream.cuda_stream))
         _lib.check(rc, f"cfg {cfg}")
@@ -92,7 +102,8 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(a.reps):
-                run(c, umem, verd)
+                rot[0] += 1
+                run(c, umem, verd, rot[0] % K)
             e1.record(stream)
             torch.cuda.synchronize()
             times[c].append(e0.elapsed_time(e1) / a.reps * 1e3)

@@ -699,7 +699,6 @@ __device__ __forceinline__ FrameRef lane_ref(const KernelArgs &a, const uint4 d,
   return make_ref(a, (static_cast<uint64_t>(d.y) << 32) | d.x, d.z, f < a.n);
 }
 
-#ifdef XSKNF_AB
 template <int NCH, int SPT>
 __global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs args) {
   constexpr uint32_t T = SPT * kWave;        // frames per tile
@@ -744,7 +743,6 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs 
   }
   publish_records(args, nrec, lane);
 }
-#endif  // XSKNF_AB
 
 // ---- split kernel: headers by lane, payload by group ----------------------------
 //
@@ -1517,14 +1515,12 @@ int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel launch");
 }
 
-#ifdef XSKNF_AB
 template <int NCH, int SPT>
 int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   auto k = checksum_kernel_lane<NCH, SPT>;
   hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, SPT * kWave)), dim3(kBlock), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
-#endif
 
 template <int W, int LPF, int NCH, int U, bool TL>
 int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
@@ -1559,6 +1555,8 @@ struct Variant {
 const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
     XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
+    // ... the lane kernel for short frames ...
+    XSKNF_L(5, 2),
     // ... and the zero-copy host path's small-batch group shapes (host_path.hip)
     XSKNF_V(32, 3, 2), XSKNF_V(64, 2, 4),
 #ifdef XSKNF_AB
@@ -1569,7 +1567,7 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
-    XSKNF_L(5, 2),     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
+    XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
     XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
@@ -1605,28 +1603,32 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   c.frames_per_group = 4;
   c.blocks_per_cu = 8;
   c.lds_ring = 0;
-  // measured best per size class on MI355X (tools/tune.py, 1M-frame batches):
-  // the split kernel with the transposed (coalesced) header-window load for
-  // every size class (group kernels in brackets).
-  //  * hint <= 128: 4-chunk window, 16 x 2 items, every check in-line (short
-  //    frames as whole 64-byte sectors, plain write-back stores: 64 B 38.1 us,
-  //    non-temporal 38.7; 570 B 142 vs 147), no scatter launch: 64 B 40 us [50];
-  //  * < 1 KiB: 8-chunk window (the frame's whole first 128-byte line, so
-  //    phase B never refetches it): 570 B 144 us [175];
+  // measured best per size class on MI355X (tools/tune.py, 1M-frame batches,
+  // launches rotating over enough batches that none is still in the 256 MiB
+  // Infinity Cache from its previous pass -- bench.py's rotation):
+  //  * hint <= 128: the lane kernel (one lane per frame, 5-chunk window), every
+  //    check in-line as its whole 64-byte sector, non-temporal: 64 B 57.6 us
+  //    [split kernel 60.3-61.3];
+  //  * < 1 KiB: the split kernel, 8-chunk window (the frame's whole first
+  //    128-byte line, so phase B never refetches it), 16 x 2 items, in-line;
+  //  * a mix of mostly short frames (mean < 1 KiB, longest >= 1 KiB: IMIX):
+  //    16 x 2 items, two in flight, every check deferred and patched by each
+  //    wave after its last tile (no second launch): IMIX 117.9 us [per-tile
+  //    policy + scatter pass 124-136, all in-line 127];
   //  * < 4 KiB: 8-chunk window, 16 x 3 items, the per-tile policy defers the
   //    checks of tiles made mostly of long frames (a uniform 1500 B batch) to
-  //    the scatter pass: 1500 B 291 us [305], IMIX 107 us [186];
+  //    the scatter pass: 1500 B 291 us [305];
   //  * jumbo: 4-chunk window, 16 x 3 items, two per group in flight: 9000 B
   //    1454 us [1540].
   c.kernel = XSKNF_GPU_KERNEL_SPLIT;
   c.lanes_per_frame = 16;
   if (hint <= 128) {
-    c.window_chunks = 4 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1 + 8;
-  } else if (hint < kDeferMinLen || (mean && mean < kDeferMinLen)) {
-    // also a mix of mostly short frames (IMIX, mean 352 B): its tiles almost
-    // never defer, so every check in-line and no scatter launch (IMIX 1M
-    // frames: 105 -> 100 us)
+    c.kernel = XSKNF_GPU_KERNEL_AUTO;
+    c.lanes_per_frame = 1; c.window_chunks = 0; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
+  } else if (hint < kDeferMinLen) {
     c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1 + 8;
+  } else if (mean && mean < kDeferMinLen) {
+    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   } else if (hint + 15 <= 4096) {
     c.window_chunks = 8 + 16; c.chunks_per_lane = 3; c.frames_per_group = 1; c.fused_stores = 0;
   } else {
