@@ -199,8 +199,8 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     # step i processes batch i % K
     umem, descs, lens = frames.device_batch(n * K, np.tile(lens_in, K), layout=layout, chunk=chunk or frames.CHUNK,
                                             seed=seed, device=dev)
-    hint, mean = int(lens.max()), int(lens.mean())      # what the caller knows of its batch
-    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint, frame_len_mean=mean)
+    hint = int(lens.max())
+    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint)
     verdicts = torch.empty(n * K, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     umem_ptr, umem_size = umem.data_ptr(), umem.numel()
@@ -261,7 +261,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     from xsknf_amd import _lib
     lib = _lib.load()
     cfg = _lib.LaunchCfg()
-    _lib.check(lib.xsknf_gpu_launch_cfg_for_lens(hint, mean, ctypes.byref(cfg)), "launch_cfg_for_lens")
+    _lib.check(lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(cfg)), "default_launch_cfg")
     single_kernel = (cfg.fused_stores & 3) == 1
     family = "checksum_kernel_split" if cfg.kernel == 1 else "checksum_kernel"
     k_ms = None

@@ -150,21 +150,6 @@ struct xsknf_gpu_launch_cfg {
 /* The shape xsknf_gpu_checksum_batch() uses for a given frame_len_hint. */
 XSKNF_GPU_API int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg);
 
-/*
- * xsknf_gpu_checksum_batch() for a caller that knows its batch's lengths: the
- * longest frame and the mean length (0 = unknown).  The mean separates a batch
- * of mostly long frames (checks of >= 1 KiB frames deferred to a write-only
- * pass, a second launch) from a mix of mostly short frames such as IMIX, whose
- * checks all go in-line in one launch.  Results are identical either way.
- */
-XSKNF_GPU_API int xsknf_gpu_checksum_batch_lens(uint8_t *umem, uint64_t umem_size,
-		const struct xsknf_gpu_desc *descs, uint32_t n,
-		uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
-		int32_t *verdicts, uint32_t frame_len_max, uint32_t frame_len_mean, void *stream);
-/* The shape xsknf_gpu_checksum_batch_lens() uses. */
-XSKNF_GPU_API int xsknf_gpu_launch_cfg_for_lens(uint32_t frame_len_max, uint32_t frame_len_mean,
-		struct xsknf_gpu_launch_cfg *cfg);
-
 /* xsknf_gpu_checksum_batch() with an explicit launch shape instead of a hint. */
 XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size,
 		const struct xsknf_gpu_desc *descs, uint32_t n,

@@ -217,6 +217,26 @@ def test_full_size_configs_bit_exact(dev, name, n, length, layout):
     assert lost.mean() < {64: 0.001, 1500: 0.01, 9000: 0.05}.get(length, 0.01)
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("length", [1500, "imix"])
+def test_batch_larger_than_one_launch(dev, length):
+    """A batch of more than 1M frames runs as consecutive launches (run() in
+    checksummer.hip): the deferred checks, record counters and verdicts of each
+    launch land on their own frames."""
+    n = (1 << 20) + 4097
+    umem, descs, lens = frames.device_batch(n, length, layout="aligned", device=dev, seed=77)
+    host = umem.cpu().numpy()
+    hd = descs.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1).copy()
+    frames.inject_edge_cases(frames.HostBatch(host, hd, "aligned"), 0.01, seed=78)
+    umem.copy_(torch.from_numpy(host))
+    descs.copy_(torch.from_numpy(hd.view(np.int64).reshape(n, 2)))
+    v = Checksummer(frame_len_hint=int(lens.max())).process_batch(umem, descs)
+    torch.cuda.synchronize()
+    _, ov = O.c_time_batch(host, hd, threads=16, reps=1)
+    assert np.array_equal(v.cpu().numpy(), ov)
+    assert np.array_equal(umem.cpu().numpy(), host)
+
+
 # lanes_per_frame, chunks_per_lane, frames_per_group, lds_ring, fused_stores[, kernel, window]
 PRODUCT_SHAPES = [
     # the split kernel shapes of default_cfg() under every store mode

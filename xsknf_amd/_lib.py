@@ -21,8 +21,6 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_last_error",
     "xsknf_gpu_default_launch_cfg",
     "xsknf_gpu_checksum_batch_cfg",
-    "xsknf_gpu_checksum_batch_lens",
-    "xsknf_gpu_launch_cfg_for_lens",
     "xsknf_gpu_ctx_create",
     "xsknf_gpu_ctx_register_umem",
     "xsknf_gpu_ctx_process_batch",
@@ -116,13 +114,6 @@ def load() -> ctypes.CDLL:
         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.POINTER(CsumOpts), ctypes.c_void_p, ctypes.POINTER(LaunchCfg), ctypes.c_void_p,
     ]
-    lib.xsknf_gpu_checksum_batch_lens.restype = ctypes.c_int
-    lib.xsknf_gpu_checksum_batch_lens.argtypes = [
-        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
-        ctypes.POINTER(CsumOpts), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
-    ]
-    lib.xsknf_gpu_launch_cfg_for_lens.restype = ctypes.c_int
-    lib.xsknf_gpu_launch_cfg_for_lens.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]
     lib.xsknf_gpu_ctx_create.restype = ctypes.c_int
     lib.xsknf_gpu_ctx_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int,
                                          ctypes.c_uint32, ctypes.c_uint32]

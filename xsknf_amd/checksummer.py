@@ -110,11 +110,10 @@ class Checksummer:
     rewritten in place in `umem` and the verdict stored in `verdicts`."""
 
     def __init__(self, options: Optional[ChecksummerOptions] = None, num_interfaces: int = 1,
-                 frame_len_hint: int = 0, frame_len_mean: int = 0):
+                 frame_len_hint: int = 0):
         self.options = options or ChecksummerOptions()
         self.num_interfaces = int(num_interfaces)
         self.frame_len_hint = int(frame_len_hint)     # longest frame (0 = unknown)
-        self.frame_len_mean = int(frame_len_mean)     # mean length (0 = unknown): mixed batches
         self._lib = _lib.load()
 
     def csum_opts(self) -> _lib.CsumOpts:
@@ -127,13 +126,6 @@ class Checksummer:
         """Raw-pointer form (device pointers), asynchronous on `stream`."""
         hint = self.frame_len_hint if frame_len_hint is None else int(frame_len_hint)
         opts = self.csum_opts()
-        if self.frame_len_mean:
-            rc = self._lib.xsknf_gpu_checksum_batch_lens(
-                ctypes.c_void_p(umem_ptr), umem_size, ctypes.c_void_p(descs_ptr), n,
-                ingress_ifindex, ctypes.byref(opts), ctypes.c_void_p(verdicts_ptr), hint, self.frame_len_mean,
-                ctypes.c_void_p(stream or None))
-            _lib.check(rc, "xsknf_gpu_checksum_batch_lens")
-            return
         rc = self._lib.xsknf_gpu_checksum_batch(
             ctypes.c_void_p(umem_ptr), umem_size, ctypes.c_void_p(descs_ptr), n,
             ingress_ifindex, ctypes.byref(opts), ctypes.c_void_p(verdicts_ptr), hint,

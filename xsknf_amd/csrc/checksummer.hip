@@ -897,51 +897,79 @@ struct ItemStage {
 // with no record costs one 256-byte read.  Per round 16 frames, 4 lanes each,
 // as the dense scatter shape: the lanes of a frame rewrite its check's 64-byte
 // sector with one non-temporal store (2 bytes where the sector leaves the frame).
+#ifndef XSKNF_TAIL_TILES
+#define XSKNF_TAIL_TILES 2
+#endif
+constexpr int kTailTiles = XSKNF_TAIL_TILES;   // tiles whose patches are in flight together
+
 __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t tile0, uint32_t waves, int lane) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int piece = lane & 3;
-  for (uint32_t tile = tile0; tile * kWave < args.n; tile += waves) {
-    const uint32_t f = tile * kWave + lane;
-    const uint32_t r = f < args.n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(args.verdicts) + f)
-                                  : 0u;
-    const bool rec = (r & kRecTagMask) == kRecTag;
-    if (!__builtin_amdgcn_ballot_w64(rec)) continue;
-    uint32_t rr[4];
-    xsknf_gpu_desc d[4];
+  constexpr int T = kTailTiles;
+  for (uint32_t tb = tile0; tb * kWave < args.n; tb += T * waves) {
+    // the records of T tiles, then their descriptors, then their sectors: three
+    // round trips for T tiles instead of two per tile
+    uint32_t r[T];
+    bool rec[T];
+    uint64_t any = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int src = 16 * k + (lane >> 2);
-      rr[k] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(r)));
-      d[k] = args.descs[min(tile * kWave + src, args.n - 1)];
-    }
-    uint4 v[4];
-    uint8_t *mine[4];
-    int o[4];
-    bool whole[4], has[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      has[k] = (rr[k] & kRecTagMask) == kRecTag;   // src < n: records exist only there
-      uint8_t *fp = args.umem + umem_offset(d[k].addr);
-      uint8_t *chk = fp + ((rr[k] >> 16) & 0x7f) + 6;
-      uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);   // keeps global addressing
-      whole[k] = has[k] && sec >= fp && sec + 64 <= fp + d[k].len && (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
-      mine[k] = whole[k] ? sec + 16 * piece : chk;
-      o[k] = static_cast<int>(chk - mine[k]);
-      if (whole[k]) v[k] = load_nt(reinterpret_cast<const uint4 *>(mine[k]));
+    for (int t = 0; t < T; ++t) {
+      const uint32_t f = (tb + t * waves) * kWave + lane;
+      r[t] = f < args.n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(args.verdicts) + f) : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint16_t c = static_cast<uint16_t>(rr[k]);
-      if (whole[k]) {
-        uint4 w = put_byte(v[k], o[k], c);
-        w = put_byte(w, o[k] + 1, c >> 8);
-        store_nt16(mine[k], w);
-      } else if (has[k] && piece == 0) {
-        mine[k][0] = static_cast<uint8_t>(c);
-        mine[k][1] = static_cast<uint8_t>(c >> 8);
+    for (int t = 0; t < T; ++t) {
+      rec[t] = (r[t] & kRecTagMask) == kRecTag;
+      any |= __builtin_amdgcn_ballot_w64(rec[t]);
+    }
+    if (!any) continue;
+    uint32_t rr[T][4];
+    xsknf_gpu_desc d[T][4];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const uint32_t tile = tb + t * waves;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int src = 16 * k + (lane >> 2);
+        rr[t][k] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(r[t])));
+        d[t][k] = args.descs[min(tile * kWave + src, args.n - 1)];
       }
     }
-    if (rec) args.verdicts[f] = args.fwd_verdict;
+    uint4 v[T][4];
+    uint8_t *mine[T][4];
+    int o[T][4];
+    bool whole[T][4], has[T][4];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        has[t][k] = (rr[t][k] & kRecTagMask) == kRecTag;   // src < n: records exist only there
+        uint8_t *fp = args.umem + umem_offset(d[t][k].addr);
+        uint8_t *chk = fp + ((rr[t][k] >> 16) & 0x7f) + 6;
+        uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);   // keeps global addressing
+        whole[t][k] = has[t][k] && sec >= fp && sec + 64 <= fp + d[t][k].len &&
+                      (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
+        mine[t][k] = whole[t][k] ? sec + 16 * piece : chk;
+        o[t][k] = static_cast<int>(chk - mine[t][k]);
+        if (whole[t][k]) v[t][k] = load_nt(reinterpret_cast<const uint4 *>(mine[t][k]));
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint16_t c = static_cast<uint16_t>(rr[t][k]);
+        if (whole[t][k]) {
+          uint4 w = put_byte(v[t][k], o[t][k], c);
+          w = put_byte(w, o[t][k] + 1, c >> 8);
+          store_nt16(mine[t][k], w);
+        } else if (has[t][k] && piece == 0) {
+          mine[t][k][0] = static_cast<uint8_t>(c);
+          mine[t][k][1] = static_cast<uint8_t>(c >> 8);
+        }
+      }
+      if (rec[t]) args.verdicts[(tb + t * waves) * kWave + lane] = args.fwd_verdict;
+    }
   }
 }
 
@@ -1597,9 +1625,8 @@ const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   return nullptr;
 }
 
-// Default shape for a batch whose longest frame is `hint` bytes and whose mean
-// length is `mean` (0 = unknown).
-void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
+// Default shape for a batch whose longest frame is `hint` bytes.
+void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
   c.frames_per_group = 4;
   c.blocks_per_cu = 8;
   c.lds_ring = 0;
@@ -1609,28 +1636,22 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   //  * hint <= 128: the lane kernel (one lane per frame, 5-chunk window), every
   //    check in-line as its whole 64-byte sector, non-temporal: 64 B 57.6 us
   //    [split kernel 60.3-61.3];
-  //  * < 1 KiB: the split kernel, 8-chunk window (the frame's whole first
-  //    128-byte line, so phase B never refetches it), 16 x 2 items, in-line;
-  //  * a mix of mostly short frames (mean < 1 KiB, longest >= 1 KiB: IMIX):
-  //    16 x 2 items, two in flight, every check deferred and patched by each
-  //    wave after its last tile (no second launch): IMIX 117.9 us [per-tile
-  //    policy + scatter pass 124-136, all in-line 127];
-  //  * < 4 KiB: 8-chunk window, 16 x 3 items, the per-tile policy defers the
-  //    checks of tiles made mostly of long frames (a uniform 1500 B batch) to
-  //    the scatter pass: 1500 B 291 us [305];
-  //  * jumbo: 4-chunk window, 16 x 3 items, two per group in flight: 9000 B
-  //    1454 us [1540].
+  //  * <= 4 KiB: the split kernel, 8-chunk window (the frame's whole first
+  //    128-byte line, so phase B never refetches it), 16 x 2 items, two in
+  //    flight, every check deferred and patched by each wave after its last
+  //    tile, two tiles' patches in flight (no second launch): 570 B 148.8 us
+  //    [in-line 170.2], IMIX 117.8 [per-tile policy + scatter pass 125-136,
+  //    all in-line 127], 1500 B 291.6-292.5 [16 x 3 items + scatter pass
+  //    294.4-297.4];
+  //  * jumbo: 4-chunk window, 16 x 3 items, two per group in flight, the
+  //    per-tile policy + scatter pass: 9000 B 1467 us [tail patches 1491].
   c.kernel = XSKNF_GPU_KERNEL_SPLIT;
   c.lanes_per_frame = 16;
   if (hint <= 128) {
     c.kernel = XSKNF_GPU_KERNEL_AUTO;
     c.lanes_per_frame = 1; c.window_chunks = 0; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
-  } else if (hint < kDeferMinLen) {
-    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 1 + 8;
-  } else if (mean && mean < kDeferMinLen) {
-    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   } else if (hint + 15 <= 4096) {
-    c.window_chunks = 8 + 16; c.chunks_per_lane = 3; c.frames_per_group = 1; c.fused_stores = 0;
+    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   } else {
     c.window_chunks = 4 + 16; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
   }
@@ -1664,6 +1685,8 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
   return 0;
 }
 
+constexpr uint32_t kLaunchFrames = 1u << 20;
+
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
   const int mode = cfg.fused_stores & 3;          // + 4: 2-byte in-line stores, + 8: plain sector stores
@@ -1678,10 +1701,23 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   // + 16: the split kernel patches its deferred checks itself (no scatter launch)
   a.tail_scatter = (cfg.fused_stores & 16) && v->kernel == XSKNF_GPU_KERNEL_SPLIT && a.defer_min_len != kNoDefer &&
                    !a.no_scatter;
-  static std::atomic<uint32_t> seq{0};
-  a.seq = seq.fetch_add(1, std::memory_order_relaxed);
   a.count_records = a.defer_min_len != kNoDefer && !a.no_scatter && !a.tail_scatter;
-  return v->fn(a, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
+  // A batch larger than kLaunchFrames runs as consecutive launches of that many
+  // frames: one launch over the whole of an 8M-frame IMIX batch (config 4 on
+  // one GPU, 16 GB of UMEM) takes 133 us per 1M frames against 113 for 1M-frame
+  // launches -- the waves' tiles drift apart over a long static schedule, and
+  // the pages in use with them.
+  static std::atomic<uint32_t> seq{0};
+  for (uint32_t off = 0; off < base.n; off += kLaunchFrames) {
+    KernelArgs p = a;
+    p.descs = base.descs + off;
+    p.verdicts = base.verdicts + off;
+    p.n = base.n - off < kLaunchFrames ? base.n - off : kLaunchFrames;
+    p.seq = seq.fetch_add(1, std::memory_order_relaxed);
+    const int rc = v->fn(p, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 }  // namespace xsknf_gpu
@@ -1723,25 +1759,6 @@ int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct
 int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg) {
   if (!cfg) return -EINVAL;
   xsknf_gpu::default_cfg(frame_len_hint ? frame_len_hint : 2048u, *cfg);
-  return 0;
-}
-
-int xsknf_gpu_checksum_batch_lens(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
-                                  uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
-                                  int32_t *verdicts, uint32_t frame_len_max, uint32_t frame_len_mean,
-                                  void *stream) {
-  xsknf_gpu::KernelArgs a;
-  const int rc = xsknf_gpu::prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
-  if (rc != 0) return rc < 0 ? rc : 0;
-  xsknf_gpu_launch_cfg cfg;
-  xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, cfg, frame_len_mean);
-  return xsknf_gpu::run(a, cfg, stream);
-}
-
-int xsknf_gpu_launch_cfg_for_lens(uint32_t frame_len_max, uint32_t frame_len_mean,
-                                  struct xsknf_gpu_launch_cfg *cfg) {
-  if (!cfg) return -EINVAL;
-  xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, *cfg, frame_len_mean);
   return 0;
 }
 

@@ -282,10 +282,8 @@ int submit_piece(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint
   memcpy(s.descs, descs, sizeof(xsknf_gpu_desc) * n);
   c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
 
-  uint64_t total = 0;   // the mean length picks a mixed batch's shape (xsknf_gpu_checksum_batch_lens)
-  for (uint32_t i = 0; i < n; ++i) total += descs[i].len;
   xsknf_gpu_launch_cfg cfg;
-  default_cfg(c->hint ? c->hint : 2048u, cfg, static_cast<uint32_t>(total / n));
+  default_cfg(c->hint ? c->hint : 2048u, cfg);
   if (c->path == XSKNF_GPU_PATH_STAGED) {
     rc = stage_frames(c, s, n, a);
     if (rc) return rc;
