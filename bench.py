@@ -262,10 +262,16 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     lib = _lib.load()
     cfg = _lib.LaunchCfg()
     _lib.check(lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(cfg)), "default_launch_cfg")
-    single_kernel = (cfg.fused_stores & 3) == 1
-    family = "checksum_kernel_split" if cfg.kernel == 1 else "checksum_kernel"
+    # one launch per step: every check in-line (mode 1), or deferred and patched
+    # by each wave after its last tile (+16, split kernel)
+    single_kernel = (cfg.fused_stores & 3) == 1 or bool(cfg.fused_stores & 16)
+    stores = ("checks in-line" if (cfg.fused_stores & 3) == 1 else
+              "checks deferred, each wave patches its own tiles" if cfg.fused_stores & 16 else
+              "checks deferred to a scatter_checks launch")
+    family = ("checksum_kernel_split" if cfg.kernel == 1 else
+              "checksum_kernel_lane" if cfg.lanes_per_frame == 1 else "checksum_kernel")
     k_ms = None
-    if primary and args.kernel_steps > 0 and not single_kernel:
+    if primary and args.kernel_steps > 0 and (cfg.fused_stores & 3) != 1:
         cfg.fused_stores = 3
         rec = torch.empty(n, dtype=torch.int32, device=dev)
         opts = cs.csum_opts()
@@ -295,7 +301,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
 
     vh = verdicts[:n].cpu().numpy()
     counters = allreduce_sum_i64([n, bytes_len, int((vh == -1).sum()), int((vh >= 0).sum())], world)
-    return dict(name=name, desc=desc, n=n, K=K, lens=lens, bytes_len=bytes_len, step_ms=step_ms,
+    return dict(name=name, desc=desc, n=n, K=K, lens=lens, bytes_len=bytes_len, step_ms=step_ms, stores=stores,
                 step_ms_max=step_ms_max,
                 sum_ms=k_ms, single_kernel=single_kernel, family=family, wall_max=wall_max, counters=counters,
                 umem=umem, descs=descs, verdicts=verdicts, sample=sample, layout=layout, chunk=chunk, span=span)
@@ -510,8 +516,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_for(args.workload),
             "basis": "whole step (SURVEY.md 8(d)): sum(len + 22) per batch / HIP-event step time on the launch "
                      "stream; traffic = FETCH_SIZE/WRITE_SIZE of every kernel of one step",
-            "kernels": (f"{prim['family']} (checks in-line)" if prim["single_kernel"]
-                        else f"{prim['family']} + scatter_checks"),
+            "kernels": f"{prim['family']} ({prim['stores']})",
             "alg_bytes_per_step": step_alg, "step_us": round(step_k_s * 1e6, 2),
             "summing_kernel_alone": kernel_alone, "attainable": attainable_for(prim)}
     cpu = None

@@ -1,22 +1,29 @@
 #!/bin/bash
-# The round's GPU evidence in one call (run ON the GPU box):
+# The round's profiling evidence in one call (run ON the GPU box):
 #   tools/prof_round.sh <tag>
-# parity tests + smoke + bench (1500 primary, all secondaries), one bench line
-# per workload as primary, rocprofv3 kernel stats of the 1500 / IMIX / 64 B
-# benches, and the FETCH_SIZE / WRITE_SIZE passes of the 1500 bench.
+# rocprofv3 kernel stats of the 1500 / IMIX / 64 B / jumbo benches, the
+# FETCH_SIZE / WRITE_SIZE passes of the 1500 / IMIX / 64 B benches, and the
+# same counters on tools/hbm_probe over known byte counts of the 1500 B and
+# 64 B access patterns (the counters' calibration for those patterns).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=${1:-round}
-OUT=$R/gpurun_out/$TAG
-mkdir -p "$OUT"
-"$R/tools/gpu_check.sh" "$TAG" || exit 1
 cd "$R"
-for W in 64 imix jumbo; do
-  timeout -k 10 240 python bench.py --workload $W --secondary "" > "$OUT/bench_$W.json" 2> "$OUT/bench_$W.err" \
-      || { echo "bench $W failed"; tail -20 "$OUT/bench_$W.err"; exit 1; }
+for W in 1500 imix 64 jumbo; do
+  "$R/tools/prof_stats.sh" "${TAG}_$W" --workload $W || { echo "prof $W failed"; exit 1; }
 done
-"$R/tools/prof_stats.sh" "${TAG}_1500" || { echo "prof 1500 failed"; exit 1; }
-"$R/tools/prof_stats.sh" "${TAG}_imix" --workload imix || { echo "prof imix failed"; exit 1; }
-"$R/tools/prof_stats.sh" "${TAG}_64" --workload 64 || { echo "prof 64 failed"; exit 1; }
-"$R/tools/prof_pmc.sh" "${TAG}_1500" || { echo "pmc 1500 failed"; exit 1; }
+for W in 1500 imix 64; do
+  "$R/tools/prof_pmc.sh" "${TAG}_$W" --workload $W || { echo "pmc $W failed"; exit 1; }
+done
+OUT=$R/gpurun_out/pmc_${TAG}_calib
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd /tmp
+for C in FETCH_SIZE WRITE_SIZE; do
+  for P in "1048576 2048 256 1504" "1048576 2048 256 64"; do
+    tag=$(echo $P | awk '{print $4}')
+    timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/${C}_$tag" -o run \
+      -- "$R/tools/build/hbm_probe" $P 5 > "$OUT/${C}_$tag.log" 2>&1 || { echo "calib $C $tag failed"; exit 1; }
+  done
+done
 echo "prof_round $TAG done"

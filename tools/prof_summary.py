@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Per-kernel durations of one bench.py run under rocprofv3 --kernel-trace
+(tools/prof_stats.sh), split the way the bench dispatches them:
+
+  * the step's kernels (warm-up + timed steps, and a scatter_checks launch per
+    step where the shape has one) -- the last --steps of them are the timed ones;
+  * the split kernel again in records-only mode (the summing pass alone,
+    bench.py's `summing_kernel_alone`): the last 3 + --kernel-steps dispatches.
+
+Prints the mean / median duration of each, to compare with the bench line's
+HIP-event figures (roofline.step_us, summing_kernel_alone.us).
+
+    python tools/prof_summary.py gpurun_out/prof_<tag> > profiles/<round>/kernels_<workload>.json
+"""
+import csv
+import json
+import os
+import statistics
+import sys
+
+
+def main():
+    d = sys.argv[1]
+    bench = json.load(open(os.path.join(d, "bench.json")))
+    steps = int(bench["steps"])
+    kalone = bench["roofline"].get("summing_kernel_alone") is not None
+    rows = []
+    for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))):
+        if "xsknf_gpu::" in r["Kernel_Name"]:
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"],
+                         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    rows.sort()
+    main_name = rows[0][1]
+    tail = 3 + 50 if kalone else 0
+    mains = [r for r in rows if r[1] == main_name]
+    step_main = mains[:len(mains) - tail] if tail else mains
+    alone = mains[len(mains) - tail:] if tail else []
+    scatter = [r for r in rows if "scatter_checks" in r[1]]
+    timed = step_main[-steps:]
+    out = {"bench_step_us": bench["roofline"]["step_us"],
+           "bench_summing_alone_us": (bench["roofline"]["summing_kernel_alone"] or {}).get("us"),
+           "kernel": main_name,
+           "step_kernel_us": {"mean": round(statistics.mean(r[2] for r in timed), 2),
+                              "median": round(statistics.median(r[2] for r in timed), 2), "n": len(timed)}}
+    if scatter:
+        ts = scatter[-steps:]
+        out["scatter_checks_us"] = {"mean": round(statistics.mean(r[2] for r in ts), 2),
+                                    "median": round(statistics.median(r[2] for r in ts), 2), "n": len(ts)}
+    if alone:
+        a = alone[3:]
+        out["records_only_us"] = {"mean": round(statistics.mean(r[2] for r in a), 2),
+                                  "median": round(statistics.median(r[2] for r in a), 2), "n": len(a)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
