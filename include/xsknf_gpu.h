@@ -166,11 +166,11 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            the frames and writes the check bytes in place
  *                            over PCIe (no copies).
  *   XSKNF_GPU_PATH_STAGED    only the batch's frame bytes are copied to a device
- *                            mirror (merged runs, one 2-D copy for frames at a
- *                            constant stride, or a CPU gather into a pinned
- *                            staging buffer for scattered frames) and
- *                            checksummed in HBM; only the 4-byte records come
- *                            back and the host writes the 2 check bytes.
+ *                            mirror (merged runs, or one 2-D copy for frames at
+ *                            a constant stride) and checksummed in HBM; only
+ *                            the 4-byte records come back and the host writes
+ *                            the 2 check bytes.  A batch of frames scattered
+ *                            over the UMEM runs as ZEROCOPY instead.
  * One context = one worker thread.  It keeps two batches in flight (two slots,
  * each with its own HIP stream): the copies and kernel of one overlap the
  * other's, and the host's share of one overlaps the device's share of the other.

@@ -10,7 +10,7 @@
 // Two batches are in flight per context: each of the two SLOTS has its own HIP
 // stream, pinned descriptor / record arrays and staging buffers, so the copies
 // and kernel of one batch overlap the other's, and the host's share of a batch
-// (copy plan, gather, writing the checks) overlaps the device's share of the
+// (copy plan, writing the checks) overlaps the device's share of the
 // other.  xsknf_gpu_ctx_submit() / _wait() expose the pipeline; the
 // synchronous xsknf_gpu_ctx_process_batch() cuts a large batch into pieces of
 // kPiece frames and runs them through the same two slots.
@@ -24,12 +24,13 @@
 //       kMergeGap share a run): a contiguous or nearly contiguous batch;
 //     - one 2-D DMA copy (row = frame, pitch = the constant stride): aligned
 //       chunks in rx order, without the gaps between frames;
-//     - a CPU gather of the frames into a pinned staging buffer, one DMA copy,
-//       and descriptors rebased onto it: a scattered batch (the fill ring hands
-//       frames back in recycled order, so a 64-frame batch can span the whole
-//       UMEM);
-//   summed in HBM with every check deferred, and only the 4-byte per-frame
-//   records come back; the host then writes each frame's 2 check bytes.
+//   and summed in HBM with every check deferred: only the 4-byte per-frame
+//   records come back and the host writes each frame's 2 check bytes.  A
+//   scattered batch (the fill ring hands frames back in recycled order, so a
+//   64-frame batch can span the whole UMEM) is instead processed exactly as
+//   ZEROCOPY does, in the mapped UMEM over PCIe (measured at 1M frames: a CPU
+//   gather into a pinned staging buffer moved 8 GB/s, CPU-bound; the mapped
+//   reads with host-applied checks 23 GB/s, host-bound; in place 41 GB/s).
 //   Copying frames back would overwrite frames outside the batch that the
 //   kernel / NIC may be filling concurrently (fill-ring frames), so it never
 //   does; the mirror is only read by the kernels, so two batches in flight may
@@ -52,8 +53,7 @@ namespace {
 constexpr int kSlots = 2;
 constexpr uint32_t kPiece = 65536;          // frames per slot submission of process_batch
 constexpr uint64_t kMergeGap = 256;         // frames closer than this share one DMA run
-constexpr size_t kMaxDmaRuns = 8;           // more runs than this (and no 2-D shape): CPU gather
-constexpr uint64_t kOutOfRange = 1ull << 47;   // an address past any UMEM: dropped untouched
+constexpr size_t kMaxDmaRuns = 8;           // more runs than this (and no 2-D shape): mapped reads
 
 struct Run {
   uint64_t off, len;
@@ -66,9 +66,6 @@ struct Slot {
   xsknf_gpu_desc *descs_mapped = nullptr;
   int32_t *rec = nullptr;                   // pinned; the kernel writes them mapped
   int32_t *rec_mapped = nullptr;
-  uint8_t *gather = nullptr;                // pinned staging buffer (STAGED, gather plan)
-  uint8_t *gather_dev = nullptr;
-  uint64_t gather_cap = 0;
   std::vector<uint64_t> offs;               // frame offsets in the host UMEM (STAGED)
   std::vector<uint32_t> order;
   std::vector<Run> runs;
@@ -78,6 +75,7 @@ struct Slot {
   uint32_t n = 0;
   int32_t *out = nullptr;
   int32_t fwd = -1;
+  bool host_checks = false;                 // records to apply on the host (STAGED, HBM mirror)
 };
 
 }  // namespace
@@ -91,6 +89,7 @@ struct xsknf_gpu_ctx {
   uint8_t *umem_host = nullptr;
   uint64_t umem_size = 0;
   uint8_t *umem_dev = nullptr;              // mapped host pointer (ZEROCOPY) or device mirror (STAGED)
+  uint8_t *umem_mapped = nullptr;           // the host UMEM mapped into the device (both paths)
   bool registered = false;
   Slot slot[kSlots];
   int next = 0;                             // slot the next piece goes to (round robin)
@@ -117,8 +116,6 @@ void release(xsknf_gpu_ctx *c) {
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.descs) (void)hipHostFree(s.descs);
     if (s.rec) (void)hipHostFree(s.rec);
-    if (s.gather) (void)hipHostFree(s.gather);
-    if (s.gather_dev) (void)hipFree(s.gather_dev);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
   if (c->registered) (void)hipHostUnregister(c->umem_host);
@@ -134,7 +131,7 @@ int complete(xsknf_gpu_ctx *c, Slot &s) {
   s.busy = false;
   hipError_t e = hipEventSynchronize(s.done);
   if (e != hipSuccess) return fail(e, "hipEventSynchronize");
-  if (c->path == XSKNF_GPU_PATH_STAGED) {
+  if (s.host_checks) {
     // checksummer_user.c:108 on the host: the 2 check bytes of every summed frame
     for (uint32_t i = 0; i < s.n; ++i) {
       const uint32_t r = static_cast<uint32_t>(s.rec[i]);
@@ -168,26 +165,9 @@ int complete_upto(xsknf_gpu_ctx *c, uint64_t upto) {
   }
 }
 
-int grow_gather(xsknf_gpu_ctx *c, Slot &s, uint64_t need) {
-  if (need <= s.gather_cap) return 0;
-  uint64_t cap = s.gather_cap ? s.gather_cap : (1u << 20);
-  while (cap < need) cap *= 2;
-  if (s.gather) (void)hipHostFree(s.gather);
-  if (s.gather_dev) (void)hipFree(s.gather_dev);
-  s.gather = nullptr;
-  s.gather_dev = nullptr;
-  s.gather_cap = 0;
-  hipError_t e = hipHostMalloc(&s.gather, cap, hipHostMallocDefault);
-  if (e == hipSuccess) e = hipMalloc(&s.gather_dev, cap + 16);   // + the last chunk's 16-byte read
-  if (e != hipSuccess) return fail(e, "staging buffer");
-  s.gather_cap = cap;
-  (void)c;
-  return 0;
-}
-
-// STAGED: move the piece's frame bytes to the device and point the kernel at
-// them.  Sets umem / umem_size of `a` (the mirror, or the slot's staging
-// buffer with the slot's descriptors rebased onto it).
+// STAGED: move the piece's frame bytes to the device mirror and point the
+// kernel at it, or (scattered frames) at the mapped host UMEM.  Returns 1 when
+// the kernel reads host memory (mapped), 0 when it reads the mirror.
 int stage_frames(xsknf_gpu_ctx *c, Slot &s, uint32_t n, xsknf_gpu::KernelArgs &a) {
   s.offs.resize(n);
   s.order.clear();
@@ -243,30 +223,30 @@ int stage_frames(xsknf_gpu_ctx *c, Slot &s, uint32_t n, xsknf_gpu::KernelArgs &a
       if (e != hipSuccess) return fail(e, "hipMemcpy2DAsync(frames)");
       moved = static_cast<uint64_t>(width) * k;
     } else {
-      // CPU gather into the pinned staging buffer (each frame keeps its 16-byte
-      // phase), one DMA copy, descriptors rebased onto the staging buffer
-      uint64_t need = 0;
-      for (uint32_t i : s.order) need = ((need + 15) & ~15ull) + 16 + s.descs[i].len;
-      int rc = grow_gather(c, s, need);
-      if (rc) return rc;
-      std::vector<uint64_t> &pos = s.offs;   // keep the host offsets: rebased copies go to descs
-      uint64_t at = 0;
-      for (uint32_t i = 0; i < n; ++i) s.descs[i].addr = kOutOfRange;
-      for (uint32_t i : s.order) {
-        at = ((at + 15) & ~15ull) + (pos[i] & 15);
-        memcpy(s.gather + at, c->umem_host + pos[i], s.descs[i].len);
-        s.descs[i].addr = at;
-        at += s.descs[i].len;
-      }
-      e = hipMemcpyAsync(s.gather_dev, s.gather, at, hipMemcpyHostToDevice, s.stream);
-      if (e != hipSuccess) return fail(e, "hipMemcpyAsync(gather)");
-      a.umem = s.gather_dev;
-      a.umem_size = at;
-      moved = at;
+      // scattered: the kernel reads the frames from the mapped UMEM over PCIe
+      a.umem = c->umem_mapped;
+      for (uint32_t i : s.order) moved += s.descs[i].len;
+      c->stats.bytes_h2d += moved;
+      return 1;
     }
   }
   c->stats.bytes_h2d += moved;
   return 0;
+}
+
+// A small batch read over PCIe is a few 64-frame tiles: the split kernel
+// would read it with a few waves.  The group kernel spreads it over many (4 or
+// 2 frames per wave), so more reads are in flight (tools/small_batch.py,
+// 1500 B: 64 frames 44.8 -> 18.8 us per call, 256: 46.8 -> 24.1, 1024:
+// 51.0 -> 45.0; equal from 4096).
+void pcie_small_batch_cfg(uint32_t n, xsknf_gpu_launch_cfg &cfg) {
+  if (n > 2048) return;
+  cfg.kernel = XSKNF_GPU_KERNEL_AUTO;
+  cfg.window_chunks = 0;
+  cfg.lds_ring = 0;
+  cfg.lanes_per_frame = n <= 256 ? 32 : 64;
+  cfg.chunks_per_lane = n <= 256 ? 3 : 2;
+  cfg.frames_per_group = n <= 256 ? 2 : 4;
 }
 
 // Enqueue one piece (n <= slot_frames) into the next slot.
@@ -284,27 +264,20 @@ int submit_piece(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint
 
   xsknf_gpu_launch_cfg cfg;
   default_cfg(c->hint ? c->hint : 2048u, cfg);
-  if (c->path == XSKNF_GPU_PATH_STAGED) {
+  bool mapped = c->path == XSKNF_GPU_PATH_ZEROCOPY;
+  if (!mapped) {
     rc = stage_frames(c, s, n, a);
-    if (rc) return rc;
-    cfg.fused_stores = 3;   // records only: the checks are applied on the host (complete())
-  } else {
-    if (n <= 2048) {
-      // A small batch is a few 64-frame tiles: the split kernel would read it
-      // over PCIe with a few waves.  The group kernel spreads it over many
-      // (4 or 2 frames per wave), so more reads are in flight
-      // (tools/small_batch.py, 1500 B: 64 frames 44.8 -> 18.8 us per call,
-      // 256: 46.8 -> 24.1, 1024: 51.0 -> 45.0; equal from 4096).
-      cfg.kernel = XSKNF_GPU_KERNEL_AUTO;
-      cfg.window_chunks = 0;
-      cfg.lds_ring = 0;
-      cfg.lanes_per_frame = n <= 256 ? 32 : 64;
-      cfg.chunks_per_lane = n <= 256 ? 3 : 2;
-      cfg.frames_per_group = n <= 256 ? 2 : 4;
-    }
+    if (rc < 0) return rc;
+    mapped = rc == 1;   // scattered frames: read (and written) in host memory, as ZEROCOPY
+  }
+  if (mapped) {
+    pcie_small_batch_cfg(n, cfg);
     cfg.fused_stores = 1;   // in place over PCIe, ...
     a.sector_stores = 0;    // ... as 2-byte writes (byte enables; no RMW in host memory)
+  } else {
+    cfg.fused_stores = 3;   // records only: the checks are applied on the host (complete())
   }
+  s.host_checks = !mapped;
   rc = run(a, cfg, s.stream);
   if (rc != 0) return rc;
   hipError_t e = hipEventRecord(s.done, s.stream);
@@ -370,23 +343,24 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
 int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *c, void *umem, uint64_t size) {
   if (!c || !umem || size == 0 || c->registered) return -EINVAL;
   hipError_t e = hipSetDevice(c->device);
-  const unsigned flags = c->path == XSKNF_GPU_PATH_ZEROCOPY ? hipHostRegisterMapped : hipHostRegisterDefault;
-  if (e == hipSuccess) e = hipHostRegister(umem, size, flags);
+  if (e == hipSuccess) e = hipHostRegister(umem, size, hipHostRegisterMapped);
   if (e != hipSuccess) return fail(e, "hipHostRegister(umem)");
   c->registered = true;
   c->umem_host = static_cast<uint8_t *>(umem);
   c->umem_size = size;
-  if (c->path == XSKNF_GPU_PATH_ZEROCOPY) {
-    void *dp = nullptr;
-    e = hipHostGetDevicePointer(&dp, umem, 0);
-    c->umem_dev = static_cast<uint8_t *>(dp);
-  } else {
-    e = hipMalloc(&c->umem_dev, size + 16);   // + the last chunk's 16-byte read
+  void *dp = nullptr;
+  e = hipHostGetDevicePointer(&dp, umem, 0);
+  c->umem_mapped = static_cast<uint8_t *>(dp);
+  if (e == hipSuccess) {
+    if (c->path == XSKNF_GPU_PATH_ZEROCOPY)
+      c->umem_dev = c->umem_mapped;
+    else
+      e = hipMalloc(&c->umem_dev, size + 16);   // + the last chunk's 16-byte read
   }
   if (e != hipSuccess) {
     (void)hipHostUnregister(umem);
     c->registered = false;
-    c->umem_dev = nullptr;
+    c->umem_dev = c->umem_mapped = nullptr;
     return fail(e, "xsknf_gpu_ctx_register_umem");
   }
   return 0;
