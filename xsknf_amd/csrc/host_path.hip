@@ -54,6 +54,7 @@ constexpr int kSlots = 2;
 constexpr uint32_t kPiece = 65536;          // frames per slot submission of process_batch
 constexpr uint64_t kMergeGap = 256;         // frames closer than this share one DMA run
 constexpr size_t kMaxDmaRuns = 8;           // more runs than this (and no 2-D shape): mapped reads
+constexpr size_t kSortMax = 4096;           // a larger batch out of address order is not sorted
 
 struct Run {
   uint64_t off, len;
@@ -181,6 +182,16 @@ int stage_frames(xsknf_gpu_ctx *c, Slot &s, uint32_t n, xsknf_gpu::KernelArgs &a
     if (off < prev) sorted = false;
     prev = off;
     s.order.push_back(i);
+  }
+  a.umem_size = c->umem_size;
+  if (!sorted && s.order.size() > kSortMax) {
+    // a large batch out of address order: scattered for every practical purpose
+    // (sorting 64K offsets costs more than reading the frames over PCIe)
+    uint64_t moved = 0;
+    for (uint32_t i : s.order) moved += s.descs[i].len;
+    c->stats.bytes_h2d += moved;
+    a.umem = c->umem_mapped;
+    return 1;
   }
   if (!sorted)
     std::sort(s.order.begin(), s.order.end(), [&](uint32_t x, uint32_t y) { return s.offs[x] < s.offs[y]; });
