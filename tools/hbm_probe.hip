@@ -223,6 +223,50 @@ __global__ __launch_bounds__(256) void scatter_rw(uint8_t *__restrict__ base, ui
   }
 }
 
+// 64-byte frames rewritten in place (the 64 B config's memory pattern): each
+// load instruction covers 16 frames, lanes 4i..4i+3 the 4 pieces of frame i
+// (one coalesced 64-B request per frame).  A wave takes K such groups per
+// round: HOLD = all K groups' loads, then all K groups' patched stores (reads
+// and writes of a wave in separate bursts); !HOLD = each group stored right
+// after its load (the store of group k overlaps the load of k+1).
+template <int K, bool HOLD, bool NT>
+__global__ __launch_bounds__(256) void probe_rw64(uint8_t *__restrict__ base, uint64_t chunks, uint32_t stride,
+                                                  uint32_t off) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const uint64_t waves = gridDim.x * 4ull;
+  const uint64_t w = blockIdx.x * 4ull + threadIdx.x / 64;
+  const uint64_t groups = (chunks + 15) / 16;
+  for (uint64_t g0 = w * K; g0 < groups; g0 += waves * K) {
+    u4v v[K];
+    if (HOLD) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint64_t f = min((g0 + k) * 16 + lane / 4, chunks - 1);
+        const u4v *a = reinterpret_cast<const u4v *>(base + f * stride + off + 16 * (lane & 3));
+        v[k] = NT ? __builtin_nontemporal_load(a) : *a;
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint64_t f = (g0 + k) * 16 + lane / 4;
+        v[k].x ^= 0x01000000u;
+        if (f < chunks) __builtin_nontemporal_store(v[k], reinterpret_cast<u4v *>(base + f * stride + off + 16 * (lane & 3)));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint64_t f = min((g0 + k) * 16 + lane / 4, chunks - 1);
+        const u4v *a = reinterpret_cast<const u4v *>(base + f * stride + off + 16 * (lane & 3));
+        v[k] = NT ? __builtin_nontemporal_load(a) : *a;
+        v[k].x ^= 0x01000000u;
+        if ((g0 + k) * 16 + lane / 4 < chunks)
+          __builtin_nontemporal_store(v[k], reinterpret_cast<u4v *>(base + f * stride + off + 16 * (lane & 3)));
+      }
+    }
+  }
+}
+
+// read-only pass of the frames of a 64-byte batch in the probe_rw64 shape
 // the same with the sector re-read non-temporal (the product's scatter pass policy)
 __global__ __launch_bounds__(256) void scatter_rw_nt(uint8_t *__restrict__ base, uint64_t chunks,
                                                      uint32_t stride, uint32_t off,
@@ -558,6 +602,33 @@ int main(int argc, char **argv) {
              (rsum + ssum) * 1e3 / (reps - 1));
     }
     CHECK(hipFree(side));
+  }
+  if (getenv("PROBE_RW64")) {
+    // 64-byte frames (off, len 64), rewritten in place: hold vs in-line, K groups
+    // of 16 frames per wave round; rotate over `rot` batches of `chunks` so the
+    // 256 MiB Infinity Cache does not keep them between launches
+    const int rot = atoi(getenv("PROBE_RW64"));
+    typedef void (*kfn)(uint8_t *, uint64_t, uint32_t, uint32_t);
+    struct { const char *name; kfn k; } ks[] = {
+        {"hold16", probe_rw64<16, true, false>}, {"hold8", probe_rw64<8, true, false>},
+        {"hold4", probe_rw64<4, true, false>},   {"inline4", probe_rw64<4, false, false>},
+        {"inline16", probe_rw64<16, false, false>}, {"hold16nt", probe_rw64<16, true, true>}};
+    for (auto &kk : ks) {
+      double best = 1e30;
+      for (int r = 0; r < 3; ++r) {
+        CHECK(hipEventRecord(e0));
+        for (int i = 0; i < reps; ++i)
+          hipLaunchKernelGGL(kk.k, dim3(cus * 4), dim3(256), 0, 0, buf + (uint64_t)(i % rot) * (chunks / rot) * stride,
+                             chunks / rot, stride, off);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms * 1e3 / reps < best ? ms * 1e3 / reps : best;
+      }
+      printf("{\"rw64\": \"%s\", \"frames_per_launch\": %llu, \"us\": %.2f}\n", kk.name,
+             (unsigned long long)(chunks / rot), best);
+    }
   }
   if (getenv("PROBE_PASS2")) {
     // Where the header sector is read: (A) the stream reads every frame byte
