@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 #include <stdint.h>
 #include <errno.h>
 #include <stdio.h>
@@ -889,6 +890,70 @@ struct ItemStage {
   }
 };
 
+// Phase B with LDS-DMA (split kernel, DMA = true): the same stages, but each
+// chunk goes straight into LDS (global_load_lds_dwordx4 ... nt: 64 lanes x 16 B
+// land contiguously at M0, lane l's at M0 + 16 l) instead of into VGPRs, and is
+// read back by the lane that requested it.  The two stages live in the wave's
+// header-window slots, dead after phase A when every check is deferred (the
+// only mode this variant runs in).  No stage registers: the kernel fits 4 waves
+// per SIMD at the 2-stage depth the register variant holds in 3.
+__device__ __forceinline__ void gload_lds_nt_asm(gchunk_ptr p, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(p), "s"(lds) : "memory", "m0");
+}
+
+template <int U, int NCH>
+struct ItemStageDMA {
+  Payload pl[U];
+  uint32_t fi[U];
+  int c0[U];
+  bool ok[U];
+  uint32_t buf;   // this stage's LDS: U * NCH KiB (wave-uniform)
+
+  template <int W, int LPF, int SPAN>
+  __device__ __forceinline__ void issue(uint32_t area, uint32_t mt, uint32_t it0, uint32_t total, int grp, int gl) {
+    constexpr int G = kWave / LPF;
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const uint32_t it = it0 + q * G + grp;
+      ok[q] = it < total;
+      const uint32_t e = lds_u16(area + 2 * min(it, total - 1));
+      fi[q] = e >> 8;
+      pl[q] = payload_of(lds_u128(mt + 16 * fi[q]));
+      c0[q] = W + static_cast<int>(e & 0xff) * SPAN;
+      if (!ok[q]) pl[q].hi = pl[q].lo;   // masked: sums nothing
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q)
+#pragma unroll
+      for (int k = 0; k < NCH; ++k)
+        gload_lds_nt_asm(pl[q].cp + min(c0[q] + k * LPF + gl, pl[q].nch - 1),
+                         __builtin_amdgcn_readfirstlane(buf + 1024 * (q * NCH + k)));
+  }
+
+  template <int N>
+  __device__ __forceinline__ void wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx950");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  }
+
+  template <int LPF>
+  __device__ __forceinline__ void consume(uint32_t ab, int gl) {
+    wait<U * NCH>();   // the other stage's DMAs stay in flight
+    const uint32_t me = buf + 16 * static_cast<uint32_t>(lane_id());
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      uint32_t blo = 0, bhi = 0;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const uint4 v = lds_u128(me + 1024 * (q * NCH + k));
+        chunk_sum_fast(v, (c0[q] + k * LPF + gl) * 16, pl[q].lo, pl[q].hi, pl[q].wl, pl[q].wh, blo, bhi);
+      }
+      const uint32_t P = group_sum_last<LPF>(blo + (bhi << 8));
+      if (gl == LPF - 1 && ok[q]) lds_add_u32(ab + 4 * fi[q], P);
+    }
+  }
+};
+
 // The deferred checks of a wave's own tiles, patched by the wave itself after
 // its last tile (KernelArgs::tail_scatter): the write-only pass of
 // scatter_checks without a second launch, and without waiting for the slowest
@@ -976,8 +1041,8 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
 // +8-11 % from 2 -> 3 waves per SIMD, so the register budget is pinned.
-template <int W, int LPF, int NCH, int U, bool TL>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U == 1 ? 4 : 1)))
+template <int W, int LPF, int NCH, int U, bool TL, bool DMA>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U == 1 || DMA ? 4 : 1)))
 void checksum_kernel_split(const KernelArgs args) {
   static_assert(W >= 4 && (W <= kHdrChunks || W == 8), "header window");
   static_assert(!TL || W == 4 || W == 8, "transposed window load: W lanes x 16 B per frame");
@@ -1125,7 +1190,15 @@ void checksum_kernel_split(const KernelArgs args) {
         for (uint32_t k = k0; __builtin_amdgcn_ballot_w64(k < k1); ++k)
           if (k < k1) lds_store_u16(iq + 2 * (start + k - r0), static_cast<uint16_t>((lane << 8) | k));
         compiler_barrier();
-        ItemStage<U, NCH> sa, sb;
+        using Stage = typename std::conditional<DMA, ItemStageDMA<U, NCH>, ItemStage<U, NCH>>::type;
+        Stage sa, sb;
+        if constexpr (DMA) {
+          static_assert(!DMA || 2 * U * NCH * 1024 <= kSlotArea, "two stages must fit the slot area");
+          sa.buf = area;
+          sb.buf = area + 1024 * U * NCH;
+          // the slots' last phase-A reads complete before the first DMA lands there
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
         sa.template issue<W, LPF, SPAN>(iq, mt, 0, nr, grp, gl);
         for (uint32_t it0 = 0;;) {
           sb.template issue<W, LPF, SPAN>(iq, mt, it0 + G * U, nr, grp, gl);
@@ -1550,9 +1623,10 @@ int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
 
-template <int W, int LPF, int NCH, int U, bool TL>
+template <int W, int LPF, int NCH, int U, bool TL, bool DMA>
 int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  auto k = checksum_kernel_split<W, LPF, NCH, U, TL>;
+  if (DMA && a.defer_min_len != 0) return -EINVAL;   // the DMA stages reuse the windows: every check deferred
+  auto k = checksum_kernel_split<W, LPF, NCH, U, TL, DMA>;
   hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave)), dim3(kBlock), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_split launch");
 }
@@ -1579,7 +1653,9 @@ struct Variant {
 #define XSKNF_L(N, S) {1, N, S, 0, &launch_lane<N, S>}
 #define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
 // split: window field = W, + 16 for the transposed (coalesced) window load
-#define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
+#define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL, false>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
+// phase B through LDS-DMA (lds_ring field = 1); every check deferred (fused_stores mode 2)
+#define XSKNF_SD(W, L, N, U) {L, N, U, 1, &launch_split<W, L, N, U, true, true>, XSKNF_GPU_KERNEL_SPLIT, W + 16}
 const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
     XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
@@ -1595,6 +1671,7 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
+    XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
@@ -1609,13 +1686,14 @@ const Variant kVariants[] = {
 #undef XSKNF_L
 #undef XSKNF_D
 #undef XSKNF_S
+#undef XSKNF_SD
 
 const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   for (const Variant &v : kVariants) {
     if (v.kernel != c.kernel) continue;
     if (v.kernel == XSKNF_GPU_KERNEL_SPLIT) {
       if (v.lpf == c.lanes_per_frame && v.nch == c.chunks_per_lane && v.u == c.frames_per_group &&
-          v.window == c.window_chunks)
+          v.window == c.window_chunks && v.ring == c.lds_ring)
         return &v;
     } else if (v.lpf == c.lanes_per_frame && v.nch == c.chunks_per_lane && v.ring == c.lds_ring &&
                (c.lds_ring || v.u == c.frames_per_group)) {
