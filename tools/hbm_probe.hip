@@ -66,6 +66,39 @@ __global__ __launch_bounds__(256) void probe(uint8_t *__restrict__ base, uint64_
   if (acc == 0x12345678u) out[0] = acc;   // keeps the loads live
 }
 
+// reads and sector writes from DIFFERENT waves of one launch: blocks [0, wb)
+// rewrite the 64-B sector holding byte off+40 of every chunk (4 lanes per
+// sector, nt, one coalesced request each), the other blocks stream every chunk's
+// bytes as probe_mode<1>.  Tells the memory-side cost of writes mixed into the
+// read stream apart from the stall a reading wave takes on its own stores.
+__global__ __launch_bounds__(256) void probe_mix(uint8_t *__restrict__ base, uint64_t pieces, uint32_t ppc,
+                                                 uint64_t chunks, uint32_t stride, uint32_t off,
+                                                 uint32_t *__restrict__ out, uint32_t wb) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  if (blockIdx.x < wb) {
+    const u4v val = {1u, 2u, 3u, 4u};
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < chunks * 4; t += wb * 256ull) {
+      uint8_t *sec = base + (((t / 4) * stride + off + 40) & ~(uint64_t)63);
+      __builtin_nontemporal_store(val, reinterpret_cast<u4v *>(sec + 16 * (t % 4)));
+    }
+    return;
+  }
+  uint32_t acc = 0;
+  const uint64_t tid = (blockIdx.x - wb) * 256ull + threadIdx.x;
+  const uint64_t nthr = (gridDim.x - wb) * 256ull;
+  for (uint64_t i = tid; i < pieces; i += 4 * nthr) {
+    u4v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t j = min(i + k * nthr, pieces - 1);
+      v[k] = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(base + (j / ppc) * stride + off + (j % ppc) * 16));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 // read variants: mode 1 = register loads with the nt (non-temporal) policy,
 // mode 2 = LDS-DMA (global_load_lds_dwordx4) default policy, mode 3 = LDS-DMA nt
 template <int MODE>
@@ -694,6 +727,28 @@ int main(int argc, char **argv) {
           CHECK(hipEventDestroy(a0)); CHECK(hipEventDestroy(a1));
         }
         printf("{\"split_K\": %u, \"head\": %u, \"total_us\": %.2f}\n", K, hd, tsum * 1e3 / (reps - 1));
+      }
+    }
+  }
+  if (getenv("PROBE_MIX")) {
+    // readers alone (writer blocks exit at once), writers alone, both in one launch
+    const uint32_t wbs[] = {64, 128, 256};
+    for (uint32_t wb : wbs) {
+      for (int m = 0; m < 3; ++m) {   // 0: readers only, 1: writers only, 2: both
+        double best = 1e30;
+        for (int r = 0; r < 3; ++r) {
+          CHECK(hipEventRecord(e0));
+          for (int i = 0; i < reps; ++i)
+            hipLaunchKernelGGL(probe_mix, dim3(m == 1 ? wb : grid + wb), dim3(256), 0, 0, buf,
+                               m == 1 ? 0 : pieces, ppc, m == 0 ? 0 : chunks, stride, off, out, wb);
+          CHECK(hipEventRecord(e1));
+          CHECK(hipEventSynchronize(e1));
+          float ms2 = 0;
+          CHECK(hipEventElapsedTime(&ms2, e0, e1));
+          best = ms2 * 1e3 / reps < best ? ms2 * 1e3 / reps : best;
+        }
+        printf("{\"mix\": \"%s\", \"writer_blocks\": %u, \"reader_blocks\": %d, \"us\": %.2f}\n",
+               m == 0 ? "readers" : (m == 1 ? "writers" : "both"), wb, m == 1 ? 0 : grid, best);
       }
     }
   }
