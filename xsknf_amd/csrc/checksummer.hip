@@ -901,6 +901,10 @@ __device__ __forceinline__ void gload_lds_nt_asm(gchunk_ptr p, uint32_t lds) {
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(p), "s"(lds) : "memory", "m0");
 }
 
+__device__ __forceinline__ void gload_lds_asm(gchunk_ptr p, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(lds) : "memory", "m0");
+}
+
 template <int U, int NCH>
 struct ItemStageDMA {
   Payload pl[U];
@@ -1041,10 +1045,11 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
 // +8-11 % from 2 -> 3 waves per SIMD, so the register budget is pinned.
-template <int W, int LPF, int NCH, int U, bool TL, bool DMA>
+template <int W, int LPF, int NCH, int U, bool TL, bool DMA, bool PFW>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U == 1 || DMA ? 4 : 1)))
 void checksum_kernel_split(const KernelArgs args) {
   static_assert(W >= 4 && (W <= kHdrChunks || W == 8), "header window");
+  static_assert(!PFW || (TL && !DMA && W == 8), "window prefetch: the transposed W = 8 layout, register phase B");
   static_assert(!TL || W == 4 || W == 8, "transposed window load: W lanes x 16 B per frame");
   static_assert(kWave % LPF == 0 && LPF >= 4, "group shape");
   constexpr int G = kWave / LPF;
@@ -1074,11 +1079,40 @@ void checksum_kernel_split(const KernelArgs args) {
   // descriptors travel two tiles ahead
   uint4 d = *reinterpret_cast<const uint4 *>(args.descs + min(tile * kWave + lane, last));
   uint4 dn = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * kWave + lane, last));
+  // PFW: the next tile's header windows go straight into the slots by LDS-DMA
+  // as soon as this tile's phase A is done with them (every check deferred: the
+  // slots are dead until then), so a tile starts on windows already in LDS.
+  // The transposed layout is the DMA's own: instruction p lands 64 x 16 B at
+  // area + 1 KiB p (kSlot = 16 W = 128: frame 8p + lane / 8, piece lane % 8).
+  const auto window_dma = [&](const uint4 dd, uint32_t ff) {
+    const FrameRef rn = lane_ref(args, dd, ff);
+    const uintptr_t cpv = reinterpret_cast<uintptr_t>(rn.cp);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slots' last reads are done
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      const int g = (kWave / W) * p + lane / W;
+      const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv)));
+      const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
+      const int nc = __builtin_amdgcn_ds_bpermute(g << 2, rn.nch);
+      const gchunk_ptr cp = reinterpret_cast<gchunk_ptr>((static_cast<uintptr_t>(hi) << 32) | lo);
+      gload_lds_asm(cp + min(lane % W, nc - 1), __builtin_amdgcn_readfirstlane(area + 1024 * p));
+    }
+  };
+  bool window_pending = false;
+  if constexpr (PFW) {
+    static_assert(!PFW || kSlot == 16 * W, "DMA layout = slot layout");
+    window_dma(d, tile * kWave + lane);
+    window_pending = true;
+  }
   for (; tile * kWave < args.n; tile += waves) {
     const uint32_t f = tile * kWave + lane;
     const FrameRef r = lane_ref(args, d, f);
     uint4 v[W];
-    if constexpr (TL) {
+    if constexpr (PFW) {
+      if (window_pending) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < W; ++k) v[k] = lds_u128(slot + 16 * k);
+    } else if constexpr (TL) {
       // transposed: lanes W*i .. W*i+W-1 load the window of frame (64/W)*p + i
       // (p = 0..W-1), one coalesced 16*W-byte request per frame instead of W
       // 16-byte ones, and drop it in that frame's slot
@@ -1168,6 +1202,10 @@ void checksum_kernel_split(const KernelArgs args) {
     }
     store_sectors(o, lane, args.plain_sector);
     const uint32_t part = h.pseudo + args.payload_mult * (PA - h.old_check);
+    if constexpr (PFW) {
+      window_pending = (tile + waves) * kWave < args.n;
+      if (window_pending) window_dma(dn, (tile + waves) * kWave + lane);
+    }
 
     // ---- phase B: payload items of the longer frames ----
     if (__builtin_amdgcn_ballot_w64(more)) {
@@ -1208,6 +1246,7 @@ void checksum_kernel_split(const KernelArgs args) {
           sb.template consume<LPF>(ab, gl);
           if ((it0 += G * U) >= nr) { sa.template wait<0>(); break; }
         }
+        window_pending = false;   // that wait<0> drained the window DMA too
       }
       // frames past the item budget: the whole wave sums each one
       for (uint64_t hm = __builtin_amdgcn_ballot_w64(huge); hm; hm &= hm - 1) {
@@ -1623,10 +1662,11 @@ int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
 
-template <int W, int LPF, int NCH, int U, bool TL, bool DMA>
+template <int W, int LPF, int NCH, int U, bool TL, bool DMA, bool PFW = false>
 int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  if (DMA && a.defer_min_len != 0) return -EINVAL;   // the DMA stages reuse the windows: every check deferred
-  auto k = checksum_kernel_split<W, LPF, NCH, U, TL, DMA>;
+  // the DMA stages / the window prefetch reuse the windows: every check deferred
+  if ((DMA || PFW) && a.defer_min_len != 0) return -EINVAL;
+  auto k = checksum_kernel_split<W, LPF, NCH, U, TL, DMA, PFW>;
   hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave)), dim3(kBlock), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_split launch");
 }
@@ -1656,6 +1696,8 @@ struct Variant {
 #define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL, false>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
 // phase B through LDS-DMA (lds_ring field = 1); every check deferred (fused_stores mode 2)
 #define XSKNF_SD(W, L, N, U) {L, N, U, 1, &launch_split<W, L, N, U, true, true>, XSKNF_GPU_KERNEL_SPLIT, W + 16}
+// header windows prefetched by LDS-DMA one tile ahead (lds_ring field = 2); every check deferred
+#define XSKNF_SP(L, N, U) {L, N, U, 2, &launch_split<8, L, N, U, true, false, true>, XSKNF_GPU_KERNEL_SPLIT, 24}
 const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
     XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
@@ -1672,6 +1714,7 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
     XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
+    XSKNF_SP(16, 2, 2), XSKNF_SP(16, 3, 1),         // window prefetch: +3-6 us on 1500 / IMIX / 570 (tune_pfw)
     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
@@ -1687,6 +1730,7 @@ const Variant kVariants[] = {
 #undef XSKNF_D
 #undef XSKNF_S
 #undef XSKNF_SD
+#undef XSKNF_SP
 
 const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   for (const Variant &v : kVariants) {
