@@ -263,6 +263,8 @@ AB_SHAPES = [
     (16, 4, 1, 0, 4, 1, 4), (16, 2, 2, 0, 0, 1, 5), (64, 2, 1, 0, 0, 1, 4), (32, 2, 1, 0, 1, 1, 4),
     (16, 2, 1, 0, 0, 1, 7), (16, 3, 1, 0, 2, 1, 4), (8, 2, 2, 0, 1, 1, 4),
     (16, 2, 1, 0, 5, 1, 20), (16, 3, 1, 0, 1, 1, 20), (16, 2, 1, 0, 1, 1, 24), (32, 3, 1, 0, 2, 1, 24),
+    # split kernel with LDS-DMA phase B (ring 1) / window prefetch (ring 2): every check deferred only
+    (16, 2, 2, 1, 18, 1, 24), (16, 4, 1, 1, 2, 1, 24), (16, 2, 2, 2, 18, 1, 24), (16, 3, 1, 2, 2, 1, 24),
 ]
 AB_BUILD = "ab" in os.path.basename(os.path.dirname(os.environ.get("XSKNF_GPU_LIB", "")))
 SHAPES = PRODUCT_SHAPES + [pytest.param(s, marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only"))
