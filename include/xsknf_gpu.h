@@ -116,10 +116,9 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * the 2 check bytes alone instead, adding 8 makes the lane kernel's sector
  * stores plain (write-back) rather than non-temporal (A/B).  Adding 16 (split
  * kernel) patches the deferred checks in the summing kernel itself, each wave
- * its own tiles after its last one, instead of a second launch: better for
- * mixed batches where few checks are deferred (IMIX 106 -> 102 us per 1M
- * frames), worse for uniform long frames (1500 B 292 -> 304 us), where the
- * patches overlap the other waves' reads.
+ * its own tiles after its last one, instead of a second launch (the default
+ * with 2 up to 4 KiB frames: every check deferred, then patched in bursts at
+ * the waves' ends).
  * `kernel` = XSKNF_GPU_KERNEL_SPLIT selects the split kernel (the default for
  * every hint): lane l of a wave parses, sums and finishes frame l of a
  * 64-frame tile from its first `window_chunks` & 15 (4..7, or 8) chunks, and the
