@@ -346,7 +346,7 @@ constexpr uint32_t kPendTag = 0x80000000u;
 #ifndef XSKNF_DEFER_MIN_LEN
 #define XSKNF_DEFER_MIN_LEN 1024
 #endif
-#ifndef XSKNF_DEFER_TILE_K   // a tile defers when K * (long frames) >= live frames
+#ifndef XSKNF_DEFER_TILE_K   // a tile defers when K * (long frames) >= live frames (0: every long frame defers)
 #define XSKNF_DEFER_TILE_K 2
 #endif
 constexpr uint32_t kDeferMinLen = XSKNF_DEFER_MIN_LEN;        // hybrid default (tools/tune.py: 64 B, 570 B
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel(const KernelArgs args)
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(lane < T && tf0 + lane < args.n && dnext.z >= args.defer_min_len)));
       const uint32_t nlive = min(static_cast<uint32_t>(T), args.n - tf0);
-      if (XSKNF_DEFER_TILE_K * nlong < nlive) ta.defer_min_len = kNoDefer;
+      if (XSKNF_DEFER_TILE_K > 0 && XSKNF_DEFER_TILE_K * nlong < nlive) ta.defer_min_len = kNoDefer;
     }
     dnext = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * T + min(lane, T - 1), last));
 
@@ -1146,7 +1146,7 @@ void checksum_kernel_split(const KernelArgs args) {
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(f < args.n && d.z >= defer_min)));
       const uint32_t nlive = min(static_cast<uint32_t>(kWave), args.n - tile * kWave);
-      if (XSKNF_DEFER_TILE_K * nlong < nlive) defer_min = kNoDefer;
+      if (XSKNF_DEFER_TILE_K > 0 && XSKNF_DEFER_TILE_K * nlong < nlive) defer_min = kNoDefer;
     }
 
     // ---- phase A: header, window sum, short frames finished ----
