@@ -39,7 +39,8 @@ $(APP): xsknf_amd/csrc/checksummer_app.c $(RTLIB) $(LIB) include/xsknf.h include
 VETH := tools/build/xsk_veth
 PROBE := tools/build/hbm_probe
 PROBELIB := tools/build/libhbm_probe.so
-tools: $(VETH) $(PROBE) $(PROBELIB)
+HOOKBENCH := tools/build/hook_bench
+tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH)
 $(PROBE): tools/hbm_probe.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Wno-inline-asm -o $@ $<
@@ -50,6 +51,13 @@ $(VETH): tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c $(RTLIB) oracle
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c \
 		-L$(LIBDIR) -lxsknf -Loracle/build -lcsum_oracle \
+		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread
+
+# NF-level rate of the worker loop with the GPU hook (one-call / two-phase) or the CPU NF
+$(HOOKBENCH): tools/hook_bench.c $(RTLIB) $(LIB) oracle
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ tools/hook_bench.c \
+		-L$(LIBDIR) -lxsknf -lxsknf_gpu -Loracle/build -lcsum_oracle \
 		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread
 
 # A/B build: every kernel family and launch shape (tools/tune.py, tools/ab_libs.sh;

@@ -118,10 +118,26 @@ typedef int (*xsknf_batch_processor_fn)(void *user, unsigned worker_idx, void *u
 		uint64_t umem_size, const struct xdp_desc *descs, uint32_t n,
 		unsigned ingress_ifindex, int32_t *verdicts);
 
-/* Select the NF: call before xsknf_start_workers().  The batch hook takes
- * precedence; with neither set, the xsknf_packet_processor symbol is used. */
+/* Two-phase batch hook: `submit` starts the NF on a batch as the one-call hook
+ * would (same arguments) and returns at once with a ticket; `complete` blocks
+ * until that batch's verdicts -- and any writes into its frames -- are done.
+ * The worker keeps one batch in flight: it submits batch k+1, then completes
+ * and routes batch k, so an accelerator's round trip overlaps the next rx.  A
+ * batch in flight is completed without waiting for more traffic when the rx
+ * ring runs dry, and before the worker stops.  The frames, descriptors and
+ * verdicts of a batch stay untouched by the runtime until its complete. */
+typedef int (*xsknf_batch_submit_fn)(void *user, unsigned worker_idx, void *umem,
+		uint64_t umem_size, const struct xdp_desc *descs, uint32_t n,
+		unsigned ingress_ifindex, int32_t *verdicts, uint64_t *ticket);
+typedef int (*xsknf_batch_complete_fn)(void *user, unsigned worker_idx, void *umem, uint64_t ticket);
+
+/* Select the NF: call before xsknf_start_workers().  A batch hook (one-call or
+ * two-phase; the last set wins) takes precedence; with neither set, the
+ * xsknf_packet_processor symbol is used. */
 XSKNF_API int xsknf_set_packet_processor(xsknf_packet_processor_fn fn);
 XSKNF_API int xsknf_set_batch_processor(xsknf_batch_processor_fn fn, void *user);
+XSKNF_API int xsknf_set_batch_processor_async(xsknf_batch_submit_fn submit,
+		xsknf_batch_complete_fn complete, void *user);
 
 /* The UMEM buffer a worker's socket on iface_idx uses (after xsknf_init). */
 XSKNF_API int xsknf_get_umem(unsigned worker_idx, unsigned iface_idx, void **buffer,

@@ -223,6 +223,16 @@ XSKNF_GPU_API int xsknf_gpu_hook_create(struct xsknf_gpu_hook **hook, const stru
 		uint32_t workers, int path, uint32_t max_batch, uint32_t frame_len_hint);
 XSKNF_GPU_API int xsknf_gpu_hook_process(void *hook, uint32_t worker_idx, void *umem, uint64_t umem_size,
 		const struct xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex, int32_t *verdicts);
+/* The same NF as a two-phase hook (xsknf_batch_submit_fn / xsknf_batch_complete_fn):
+ *   xsknf_set_batch_processor_async((xsknf_batch_submit_fn)xsknf_gpu_hook_submit,
+ *                                   (xsknf_batch_complete_fn)xsknf_gpu_hook_complete, hook);
+ * submit enqueues the batch on the worker's context (xsknf_gpu_ctx_submit),
+ * complete waits for its ticket (xsknf_gpu_ctx_wait): the worker receives the
+ * next batch while the GPU checksums this one. */
+XSKNF_GPU_API int xsknf_gpu_hook_submit(void *hook, uint32_t worker_idx, void *umem, uint64_t umem_size,
+		const struct xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex, int32_t *verdicts,
+		uint64_t *ticket);
+XSKNF_GPU_API int xsknf_gpu_hook_complete(void *hook, uint32_t worker_idx, void *umem, uint64_t ticket);
 /* Sum of the worker's context stats. */
 XSKNF_GPU_API int xsknf_gpu_hook_get_stats(const struct xsknf_gpu_hook *hook, uint32_t worker_idx,
 		struct xsknf_gpu_ctx_stats *stats);

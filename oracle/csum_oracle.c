@@ -223,3 +223,83 @@ int oracle_nf_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex
 {
 	return oracle_packet_processor(pkt, len, ingress_ifindex, &nf_opts);
 }
+
+/* ---- the same NF as a two-phase batch hook (runtime tests) ----------
+ * xsknf_batch_submit_fn / xsknf_batch_complete_fn for the runtime's
+ * xsknf_set_batch_processor_async: submit only records the batch; complete
+ * runs the per-frame oracle over every recorded batch up to its ticket.  So a
+ * runtime that touched a batch's frames, descriptors or verdicts before its
+ * complete would route frames on unset verdicts, and the tests see it.
+ * oracle_nf_async_stats() counts submits made while another batch of the
+ * worker was still recorded (the overlap the two-phase hook exists for). */
+#define ORACLE_ASYNC_DEPTH 8
+#define ORACLE_ASYNC_WORKERS 64
+
+struct oracle_async_batch {
+	uint8_t *umem;
+	const struct oracle_desc *descs;
+	uint32_t n;
+	uint32_t ingress;
+	int32_t *verdicts;
+	uint64_t ticket;
+};
+
+static struct {
+	struct oracle_async_batch q[ORACLE_ASYNC_DEPTH];
+	unsigned head, count;
+	uint64_t next;
+	uint64_t submits, overlapped;
+} oracle_async[ORACLE_ASYNC_WORKERS];
+
+int oracle_nf_batch_submit(void *user, unsigned worker, void *umem, uint64_t umem_size,
+		const struct oracle_desc *descs, uint32_t n, unsigned ingress, int32_t *verdicts,
+		uint64_t *ticket)
+{
+	(void)user;
+	(void)umem_size;
+	if (worker >= ORACLE_ASYNC_WORKERS || !ticket)
+		return -22;
+	typeof(oracle_async[0]) *a = &oracle_async[worker];
+	if (a->count == ORACLE_ASYNC_DEPTH)
+		return -16;
+	a->submits++;
+	if (a->count)
+		a->overlapped++;
+	struct oracle_async_batch *b = &a->q[(a->head + a->count++) % ORACLE_ASYNC_DEPTH];
+	*b = (struct oracle_async_batch){umem, descs, n, ingress, verdicts, ++a->next};
+	for (uint32_t i = 0; i < n; i++)
+		verdicts[i] = 0x7eadbeef;    /* "not computed yet" */
+	*ticket = b->ticket;
+	return 0;
+}
+
+int oracle_nf_batch_complete(void *user, unsigned worker, void *umem, uint64_t ticket)
+{
+	(void)user;
+	(void)umem;
+	if (worker >= ORACLE_ASYNC_WORKERS)
+		return -22;
+	typeof(oracle_async[0]) *a = &oracle_async[worker];
+	while (a->count && a->q[a->head].ticket <= ticket) {
+		const struct oracle_async_batch *b = &a->q[a->head];
+		for (uint32_t i = 0; i < b->n; i++)
+			b->verdicts[i] = oracle_packet_processor(b->umem + umem_offset(b->descs[i].addr),
+					b->descs[i].len, b->ingress, &nf_opts);
+		a->head = (a->head + 1) % ORACLE_ASYNC_DEPTH;
+		a->count--;
+	}
+	return 0;
+}
+
+void oracle_nf_async_stats(unsigned worker, uint64_t *submits, uint64_t *overlapped)
+{
+	if (worker >= ORACLE_ASYNC_WORKERS)
+		return;
+	*submits = oracle_async[worker].submits;
+	*overlapped = oracle_async[worker].overlapped;
+}
+
+void oracle_nf_async_reset(void)
+{
+	memset(oracle_async, 0, sizeof(oracle_async));
+}

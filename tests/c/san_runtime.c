@@ -30,6 +30,10 @@ struct oracle_opts {
 int oracle_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex, const struct oracle_opts *o);
 void oracle_nf_set_options(int32_t csum_iterations, int32_t action, uint32_t num_interfaces);
 int oracle_nf_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex);
+/* the same NF as a two-phase hook (argv[2] == "async": one batch in flight per worker) */
+int oracle_nf_batch_submit(void *user, unsigned worker, void *umem, uint64_t umem_size,
+		const struct xdp_desc *descs, uint32_t n, unsigned ingress, int32_t *verdicts, uint64_t *ticket);
+int oracle_nf_batch_complete(void *user, unsigned worker, void *umem, uint64_t ticket);
 
 #define WORKERS 2
 #define IFACES 2
@@ -90,7 +94,10 @@ int main(int argc, char **argv)
 		return 2;
 	}
 	oracle_nf_set_options(1, action, IFACES);
-	xsknf_set_packet_processor(oracle_nf_packet_processor);
+	if (argc > 2 && !strcmp(argv[2], "async"))
+		xsknf_set_batch_processor_async(oracle_nf_batch_submit, oracle_nf_batch_complete, NULL);
+	else
+		xsknf_set_packet_processor(oracle_nf_packet_processor);
 	for (int w = 0; w < WORKERS; w++)
 		for (int i = 0; i < IFACES; i++) {
 			orig[w][i] = malloc((size_t)NFRAMES * STRIDE);

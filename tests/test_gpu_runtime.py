@@ -23,12 +23,15 @@ def frames():
     return config1.frames_check(9000)
 
 
-def run_loop(cfg, plan, n_if=1, **hook_kw):
+def run_loop(cfg, plan, n_if=1, two_phase=False, **hook_kw):
     hook = R.GpuHook(workers=cfg.workers, max_batch=cfg.batch_size, num_interfaces=n_if,
                      frame_len_hint=cfg.xsk_frame_size, **hook_kw)
     rt = R.Runtime(cfg)
     try:
-        rt.set_batch_processor(hook.fn_ptr, hook.handle)
+        if two_phase:   # xsknf_gpu_hook_submit / _complete: one batch in flight per worker
+            rt.set_batch_processor_async(hook.submit_ptr, hook.complete_ptr, hook.handle)
+        else:
+            rt.set_batch_processor(hook.fn_ptr, hook.handle)
         rt.start()
         got = pump(rt, plan, n_if=n_if, timeout=60)
         assert rt.stop() == 0
@@ -41,11 +44,12 @@ def run_loop(cfg, plan, n_if=1, **hook_kw):
     return got, hs, st
 
 
+@pytest.mark.parametrize("two_phase", [False, True], ids=["one-call", "two-phase"])
 @pytest.mark.parametrize("path", [_lib.PATH_ZEROCOPY, _lib.PATH_STAGED], ids=["zerocopy", "staged"])
 @pytest.mark.parametrize("batch", [64, 2048])
-def test_gpu_hook_redirect_matches_oracle(frames, path, batch):
+def test_gpu_hook_redirect_matches_oracle(frames, path, batch, two_phase):
     cfg = R.make_config(["emu0"], batch_size=batch)
-    got, hs, st = run_loop(cfg, {0: frames}, path=path, iterations=2)
+    got, hs, st = run_loop(cfg, {0: frames}, two_phase=two_phase, path=path, iterations=2)
     want = [b for v, b in expected(frames, iterations=2) if v != -1]
     assert got[0] == want
     assert hs["frames"] == len(frames) == st[0]["rx_npkts"]
@@ -65,11 +69,12 @@ def test_gpu_hook_unaligned(frames):
     assert got[0] == [b for v, b in expected(frames[:6000], iterations=5) if v != -1]
 
 
+@pytest.mark.parametrize("two_phase", [False, True], ids=["one-call", "two-phase"])
 @pytest.mark.parametrize("bind", [(0, 0), (R.XDP_COPY, R.XDP_ZEROCOPY)], ids=["shared-umem", "two-umems"])
-def test_gpu_hook_two_interfaces(frames, bind):
+def test_gpu_hook_two_interfaces(frames, bind, two_phase):
     f0, f1 = frames[:4000], frames[4000:8000]
     cfg = R.make_config(["emu0", "emu1"], batch_size=256, bind=list(bind))
-    got, _, _ = run_loop(cfg, {0: f0, 1: f1}, n_if=2)
+    got, _, _ = run_loop(cfg, {0: f0, 1: f1}, n_if=2, two_phase=two_phase)
     e0, e1 = expected(f0, 0, nif=2), expected(f1, 1, nif=2)
     assert sorted(got[0]) == sorted([b for v, b in e0 + e1 if v == 0])
     assert sorted(got[1]) == sorted([b for v, b in e0 + e1 if v == 1])

@@ -1,7 +1,8 @@
 """The host runtime (libxsknf's C sources) and the CPU oracle under
 ThreadSanitizer and AddressSanitizer + UBSan: two worker
-threads, two emulated interfaces, REDIRECT and DROP, checked frame by frame
-against the oracle (tests/c/san_runtime.c).  CPU only."""
+threads, two emulated interfaces, REDIRECT and DROP, the per-frame NF and the
+two-phase batch hook, checked frame by frame against the oracle
+(tests/c/san_runtime.c).  CPU only."""
 import os
 import shutil
 import subprocess
@@ -30,9 +31,12 @@ def builds(tmp_path_factory):
 
 @pytest.mark.parametrize("san", ["tsan", "asan"])
 @pytest.mark.parametrize("action", ["redirect", "drop"])
-def test_runtime_is_sanitizer_clean(builds, san, action):
+@pytest.mark.parametrize("hook", ["per-frame", "async"])
+def test_runtime_is_sanitizer_clean(builds, san, action, hook):
+    """hook "async": the two-phase batch hook (one batch in flight per worker)."""
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1")
-    r = subprocess.run([builds[san], action], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([builds[san], action, hook], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
     assert "bad 0" in r.stdout

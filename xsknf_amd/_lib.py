@@ -30,6 +30,8 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_ctx_destroy",
     "xsknf_gpu_hook_create",
     "xsknf_gpu_hook_process",
+    "xsknf_gpu_hook_submit",
+    "xsknf_gpu_hook_complete",
     "xsknf_gpu_hook_get_stats",
     "xsknf_gpu_hook_destroy",
 )
@@ -139,6 +141,12 @@ def load() -> ctypes.CDLL:
     lib.xsknf_gpu_hook_process.restype = ctypes.c_int
     lib.xsknf_gpu_hook_process.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    lib.xsknf_gpu_hook_submit.restype = ctypes.c_int
+    lib.xsknf_gpu_hook_submit.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_uint64)]
+    lib.xsknf_gpu_hook_complete.restype = ctypes.c_int
+    lib.xsknf_gpu_hook_complete.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
     lib.xsknf_gpu_hook_get_stats.restype = ctypes.c_int
     lib.xsknf_gpu_hook_get_stats.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(CtxStats)]
     lib.xsknf_gpu_hook_destroy.restype = ctypes.c_int

@@ -38,6 +38,7 @@ static int opt_action = XSKNF_CSUM_ACTION_REDIRECT;
 static int opt_csum_iterations = 1;
 static int opt_quiet, opt_extra_stats, opt_app_stats;
 static int opt_gpu_path = XSKNF_GPU_PATH_ZEROCOPY;
+static int opt_gpu_sync;
 static unsigned long opt_gen_count;
 static unsigned opt_gen_len = 64;
 static volatile sig_atomic_t benchmark_done, stats_requested;
@@ -50,6 +51,7 @@ static const struct option long_options[] = {
 	{"extra-stats", no_argument, 0, 'x'},
 	{"app-stats", no_argument, 0, 'a'},
 	{"gpu-path", required_argument, 0, 'g'},
+	{"gpu-sync", no_argument, 0, 's'},
 	{"emu-gen", required_argument, 0, 'G'},
 	{0, 0, 0, 0},
 };
@@ -65,6 +67,8 @@ static void usage(const char *prog)
 		"  -x, --extra-stats	Display extra statistics.\n"
 		"  -a, --app-stats	Display application (syscall) statistics.\n"
 		"  -g, --gpu-path	ZEROCOPY (default) or STAGED host path to the GPU.\n"
+		"  -s, --gpu-sync	One batch at a time (default: the next batch is received\n"
+		"			while the GPU checksums the last one).\n"
 		"  -G, --emu-gen		COUNT[:LEN] frames per emulated queue from a built-in generator.\n"
 		"\n",
 		prog);
@@ -74,7 +78,7 @@ static void usage(const char *prog)
 static void parse_command_line(int argc, char **argv, char *app_path)
 {
 	int option_index, c;
-	while ((c = getopt_long(argc, argv, "qxai:c:g:G:", long_options, &option_index)) != -1) {
+	while ((c = getopt_long(argc, argv, "qxasi:c:g:G:", long_options, &option_index)) != -1) {
 		switch (c) {
 		case 'c':
 			if (!strcmp(optarg, "REDIRECT")) {
@@ -97,6 +101,9 @@ static void parse_command_line(int argc, char **argv, char *app_path)
 			break;
 		case 'a':
 			opt_app_stats = 1;
+			break;
+		case 's':
+			opt_gpu_sync = 1;
 			break;
 		case 'g':
 			if (!strcmp(optarg, "ZEROCOPY")) {
@@ -330,7 +337,11 @@ int main(int argc, char **argv)
 		xsknf_cleanup();
 		return EXIT_FAILURE;
 	}
-	xsknf_set_batch_processor((xsknf_batch_processor_fn)xsknf_gpu_hook_process, hook);
+	if (opt_gpu_sync)
+		xsknf_set_batch_processor((xsknf_batch_processor_fn)xsknf_gpu_hook_process, hook);
+	else
+		xsknf_set_batch_processor_async((xsknf_batch_submit_fn)xsknf_gpu_hook_submit,
+				(xsknf_batch_complete_fn)xsknf_gpu_hook_complete, hook);
 	rc = xsknf_start_workers();
 	if (rc) {
 		fprintf(stderr, "ERROR: xsknf_start_workers: %s\n", strerror(-rc));

@@ -475,41 +475,77 @@ int xsknf_gpu_hook_create(struct xsknf_gpu_hook **out, const struct xsknf_csum_o
   return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+// The worker's context for `umem`, created and registered on first use
+// (umem_size == 0: look up only).
+int hook_ctx(xsknf_gpu_hook *h, uint32_t worker_idx, void *umem, uint64_t umem_size, xsknf_gpu_ctx **out) {
+  if (!h || worker_idx >= h->workers || !umem) return -EINVAL;
+  HookWorker &w = h->w[worker_idx];
+  for (HookSlot &s : w.slot) {
+    if (s.umem == umem) {
+      *out = s.ctx;
+      return 0;
+    }
+  }
+  if (umem_size == 0) return -ENOENT;
+  HookSlot *free_slot = nullptr;
+  for (HookSlot &s : w.slot) {
+    if (!s.umem) {
+      free_slot = &s;
+      break;
+    }
+  }
+  if (!free_slot) return -ENOSPC;
+  xsknf_gpu_ctx *ctx = nullptr;
+  int rc = xsknf_gpu_ctx_create(&ctx, static_cast<int>(worker_idx % static_cast<uint32_t>(h->devices)), h->path,
+                                h->max_batch, h->hint);
+  if (rc) return rc;
+  rc = xsknf_gpu_ctx_register_umem(ctx, umem, umem_size);
+  if (rc) {
+    xsknf_gpu_ctx_destroy(ctx);
+    return rc;
+  }
+  free_slot->umem = umem;
+  free_slot->ctx = ctx;
+  *out = ctx;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
 int xsknf_gpu_hook_process(void *hook, uint32_t worker_idx, void *umem, uint64_t umem_size,
                            const struct xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
                            int32_t *verdicts) {
   xsknf_gpu_hook *h = static_cast<xsknf_gpu_hook *>(hook);
-  if (!h || worker_idx >= h->workers || !umem || umem_size == 0) return -EINVAL;
-  if (n > h->max_batch) return -EINVAL;
-  HookWorker &w = h->w[worker_idx];
+  if (!h || umem_size == 0 || n > h->max_batch) return -EINVAL;
   xsknf_gpu_ctx *ctx = nullptr;
-  for (HookSlot &s : w.slot) {
-    if (s.umem == umem) {
-      ctx = s.ctx;
-      break;
-    }
-  }
-  if (!ctx) {
-    HookSlot *free_slot = nullptr;
-    for (HookSlot &s : w.slot) {
-      if (!s.umem) {
-        free_slot = &s;
-        break;
-      }
-    }
-    if (!free_slot) return -ENOSPC;
-    int rc = xsknf_gpu_ctx_create(&ctx, static_cast<int>(worker_idx % static_cast<uint32_t>(h->devices)),
-                                  h->path, h->max_batch, h->hint);
-    if (rc) return rc;
-    rc = xsknf_gpu_ctx_register_umem(ctx, umem, umem_size);
-    if (rc) {
-      xsknf_gpu_ctx_destroy(ctx);
-      return rc;
-    }
-    free_slot->umem = umem;
-    free_slot->ctx = ctx;
-  }
+  const int rc = hook_ctx(h, worker_idx, umem, umem_size, &ctx);
+  if (rc) return rc;
   return xsknf_gpu_ctx_process_batch(ctx, descs, n, ingress_ifindex, &h->opts, verdicts);
+}
+
+int xsknf_gpu_hook_submit(void *hook, uint32_t worker_idx, void *umem, uint64_t umem_size,
+                          const struct xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
+                          int32_t *verdicts, uint64_t *ticket) {
+  xsknf_gpu_hook *h = static_cast<xsknf_gpu_hook *>(hook);
+  if (!h || umem_size == 0 || n > h->max_batch || !ticket) return -EINVAL;
+  xsknf_gpu_ctx *ctx = nullptr;
+  const int rc = hook_ctx(h, worker_idx, umem, umem_size, &ctx);
+  if (rc) return rc;
+  return xsknf_gpu_ctx_submit(ctx, descs, n, ingress_ifindex, &h->opts, verdicts, ticket);
+}
+
+int xsknf_gpu_hook_complete(void *hook, uint32_t worker_idx, void *umem, uint64_t ticket) {
+  xsknf_gpu_hook *h = static_cast<xsknf_gpu_hook *>(hook);
+  xsknf_gpu_ctx *ctx = nullptr;
+  const int rc = hook_ctx(h, worker_idx, umem, 0, &ctx);
+  if (rc) return rc;
+  return xsknf_gpu_ctx_wait(ctx, ticket);
 }
 
 int xsknf_gpu_hook_get_stats(const struct xsknf_gpu_hook *h, uint32_t worker_idx, struct xsknf_gpu_ctx_stats *stats) {

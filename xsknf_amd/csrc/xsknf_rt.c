@@ -108,6 +108,13 @@ struct worker {
 	// per-batch scratch, sized by batch_size at init
 	struct xdp_desc *descs;
 	int32_t *verdicts;
+	// two-phase hook: the batch in flight (its own descriptor / verdict arrays;
+	// descs / verdicts above take the next one, and the two swap)
+	struct xdp_desc *pend_descs;
+	int32_t *pend_verdicts;
+	uint32_t pend_n;                     // 0: none in flight
+	unsigned pend_if;                    // the rx interface it came from
+	uint64_t pend_ticket;
 	struct pkt_info *to_drop;
 	struct pkt_info *to_tx;              // [num_interfaces][batch_size]
 	uint32_t *ntx;
@@ -140,6 +147,8 @@ static struct iface *ifaces;
 static xsknf_packet_processor_fn packet_fn;
 static xsknf_batch_processor_fn batch_fn;
 static void *batch_user;
+static xsknf_batch_submit_fn submit_fn;
+static xsknf_batch_complete_fn complete_fn;
 
 static inline uint64_t addr_offset(uint64_t addr)
 {
@@ -472,19 +481,27 @@ static int complete_tx(struct xsk_sock *xsks, unsigned ifindex)
 	return 0;
 }
 
-// run the NF over the rcvd descriptors at ring index idx: verdicts[] out
-static int run_nf(struct xsk_sock *rx, uint32_t idx, uint32_t rcvd, unsigned ingress)
+// Take the rcvd descriptors at ring index idx out of the rx ring into
+// w->descs (the frames stay the worker's until they go to a tx or fill ring).
+static void take_rx(struct xsk_sock *rx, uint32_t idx, uint32_t rcvd)
 {
 	struct worker *w = rx->worker;
-	if (batch_fn) {
-		for (uint32_t i = 0; i < rcvd; i++)
-			w->descs[i] = *ring_desc(&rx->rx, idx + i);
+	for (uint32_t i = 0; i < rcvd; i++)
+		w->descs[i] = *ring_desc(&rx->rx, idx + i);
+	ring_release(&rx->rx, rcvd);
+	rx->stats.rx_npkts += rcvd;
+}
+
+// run the NF over w->descs[0, rcvd): verdicts[] out
+static int run_nf(struct xsk_sock *rx, uint32_t rcvd, unsigned ingress)
+{
+	struct worker *w = rx->worker;
+	if (batch_fn)
 		return batch_fn(batch_user, w->id, rx->buffer, umem_bufsize, w->descs, rcvd, ingress,
 				w->verdicts);
-	}
 	xsknf_packet_processor_fn fn = packet_fn ? packet_fn : xsknf_packet_processor;
 	for (uint32_t i = 0; i < rcvd; i++) {
-		const struct xdp_desc *d = ring_desc(&rx->rx, idx + i);
+		const struct xdp_desc *d = &w->descs[i];
 		w->verdicts[i] = fn(rx->buffer + addr_offset(d->addr), d->len, ingress);
 	}
 	return 0;
@@ -526,33 +543,21 @@ static int abandon_tx(struct xsk_sock *rx, const struct pkt_info *p, uint32_t n)
 	return rx->worker->err ? rx->worker->err : rc;
 }
 
-// process_batch_1if (src/xsknf.c:630-714)
-static int process_batch_1if(struct xsk_sock *s)
+// The tx / fill half of process_batch_1if (src/xsknf.c:674-714) for a batch
+// whose verdicts are known.
+static int dispose_1if(struct xsk_sock *s, const struct xdp_desc *descs, const int32_t *verdicts,
+		       uint32_t rcvd)
 {
 	struct worker *w = s->worker;
-	int rc = complete_tx_1if(s);
-	if (rc)
-		return rc;
-	uint32_t idx;
-	const uint32_t rcvd = ring_peek(&s->rx, conf.batch_size, &idx);
-	if (!rcvd) {
-		rx_empty(s);
-		return 0;
-	}
-	rc = run_nf(s, idx, rcvd, 0);
-	if (rc)
-		return rc;
-	uint32_t ndrop = 0, ntx = 0;
+	uint32_t ndrop = 0, ntx = 0, idx;
+	int rc;
 	for (uint32_t i = 0; i < rcvd; i++) {
-		const struct xdp_desc *d = ring_desc(&s->rx, idx + i);
-		struct pkt_info p = {d->addr, d->len};
-		if (w->verdicts[i] == -1)
+		struct pkt_info p = {descs[i].addr, descs[i].len};
+		if (verdicts[i] == -1)
 			w->to_drop[ndrop++] = p;
 		else
 			w->to_tx[ntx++] = p;    // any other verdict: the one tx queue
 	}
-	ring_release(&s->rx, rcvd);
-	s->stats.rx_npkts += rcvd;
 	if ((rc = recycle_drops(s, ndrop)))
 		return rc;
 	if (ntx) {
@@ -578,37 +583,25 @@ static int process_batch_1if(struct xsk_sock *s)
 	return 0;
 }
 
-// process_batch (src/xsknf.c:476-585): per-destination tx, cross-UMEM copies
-static int process_batch(struct xsk_sock *xsks, unsigned ifindex)
+// The tx / fill half of process_batch (src/xsknf.c:500-585): per-destination
+// tx, cross-UMEM copies.
+static int dispose_multi(struct xsk_sock *xsks, unsigned ifindex, const struct xdp_desc *descs,
+			 const int32_t *verdicts, uint32_t rcvd)
 {
 	struct xsk_sock *rx = &xsks[ifindex];
 	struct worker *w = rx->worker;
 	const unsigned nif = conf.num_interfaces;
-	int rc = complete_tx(xsks, ifindex);
-	if (rc)
-		return rc;
-	uint32_t idx;
-	const uint32_t rcvd = ring_peek(&rx->rx, conf.batch_size, &idx);
-	if (!rcvd) {
-		rx_empty(rx);
-		return 0;
-	}
-	rc = run_nf(rx, idx, rcvd, ifindex);
-	if (rc)
-		return rc;
-	uint32_t ndrop = 0;
+	uint32_t ndrop = 0, idx;
+	int rc;
 	memset(w->ntx, 0, sizeof(uint32_t) * nif);
 	for (uint32_t i = 0; i < rcvd; i++) {
-		const struct xdp_desc *d = ring_desc(&rx->rx, idx + i);
-		struct pkt_info p = {d->addr, d->len};
-		const int32_t v = w->verdicts[i];
+		struct pkt_info p = {descs[i].addr, descs[i].len};
+		const int32_t v = verdicts[i];
 		if (v < 0 || (unsigned)v >= nif)
 			w->to_drop[ndrop++] = p;
 		else
 			w->to_tx[(unsigned)v * conf.batch_size + w->ntx[v]++] = p;
 	}
-	ring_release(&rx->rx, rcvd);
-	rx->stats.rx_npkts += rcvd;
 	if ((rc = recycle_drops(rx, ndrop)))
 		return rc;
 	for (unsigned i = 0; i < nif; i++) {
@@ -662,6 +655,83 @@ static int process_batch(struct xsk_sock *xsks, unsigned ifindex)
 	return 0;
 }
 
+static int dispose(struct xsk_sock *xsks, unsigned ifindex, const struct xdp_desc *descs,
+		   const int32_t *verdicts, uint32_t n)
+{
+	return conf.num_interfaces > 1 ? dispose_multi(xsks, ifindex, descs, verdicts, n)
+				       : dispose_1if(&xsks[ifindex], descs, verdicts, n);
+}
+
+// The batch in flight (two-phase hook): wait for its verdicts, then route it.
+static int finish_pending(struct worker *w)
+{
+	if (!w->pend_n)
+		return 0;
+	struct xsk_sock *rx = &w->xsks[w->pend_if];
+	const uint32_t n = w->pend_n;
+	w->pend_n = 0;
+	int rc = complete_fn(batch_user, w->id, rx->buffer, w->pend_ticket);
+	if (rc) {
+		// verdicts unknown: the frames go back to the rx socket's fill ring
+		struct pkt_info *p = w->to_drop;
+		for (uint32_t i = 0; i < n; i++)
+			p[i] = (struct pkt_info){w->pend_descs[i].addr, w->pend_descs[i].len};
+		recycle_pkts(rx, p, n);
+		return rc;
+	}
+	return dispose(w->xsks, w->pend_if, w->pend_descs, w->pend_verdicts, n);
+}
+
+// One rx batch of interface ifindex (process_batch_1if / process_batch,
+// src/xsknf.c:630-714, :478-585).  With the two-phase hook the batch is
+// submitted, and the previous one -- submitted on the last call -- is
+// completed and routed while this one runs.
+static int process_rx(struct xsk_sock *xsks, unsigned ifindex)
+{
+	struct xsk_sock *rx = &xsks[ifindex];
+	struct worker *w = rx->worker;
+	int rc = conf.num_interfaces > 1 ? complete_tx(xsks, ifindex) : complete_tx_1if(rx);
+	if (rc)
+		return rc;
+	uint32_t idx;
+	const uint32_t rcvd = ring_peek(&rx->rx, conf.batch_size, &idx);
+	if (!rcvd) {
+		// nothing new: the batch in flight is not held back waiting for traffic
+		if ((rc = finish_pending(w)))
+			return rc;
+		rx_empty(rx);
+		return 0;
+	}
+	take_rx(rx, idx, rcvd);
+	if (!submit_fn) {
+		if ((rc = run_nf(rx, rcvd, ifindex)))
+			return rc;
+		return dispose(xsks, ifindex, w->descs, w->verdicts, rcvd);
+	}
+	uint64_t ticket = 0;
+	rc = submit_fn(batch_user, w->id, rx->buffer, umem_bufsize, w->descs, rcvd, ifindex, w->verdicts,
+		       &ticket);
+	if (rc) {
+		struct pkt_info *p = w->to_drop;
+		for (uint32_t i = 0; i < rcvd; i++)
+			p[i] = (struct pkt_info){w->descs[i].addr, w->descs[i].len};
+		recycle_pkts(rx, p, rcvd);
+		return rc;
+	}
+	rc = finish_pending(w);
+	// the new batch becomes the one in flight; its arrays swap with the scratch
+	struct xdp_desc *d = w->pend_descs;
+	int32_t *v = w->pend_verdicts;
+	w->pend_descs = w->descs;
+	w->pend_verdicts = w->verdicts;
+	w->descs = d;
+	w->verdicts = v;
+	w->pend_n = rcvd;
+	w->pend_if = ifindex;
+	w->pend_ticket = ticket;
+	return rc;
+}
+
 // worker_loop (src/xsknf.c:716-742)
 static void *worker_loop(void *arg)
 {
@@ -683,15 +753,16 @@ static void *worker_loop(void *arg)
 				continue;
 		}
 		int rc = 0;
-		if (conf.num_interfaces > 1) {
-			for (unsigned i = 0; i < conf.num_interfaces && !rc; i++)
-				rc = process_batch(w->xsks, i);
-		} else {
-			rc = process_batch_1if(&w->xsks[0]);
-		}
+		for (unsigned i = 0; i < conf.num_interfaces && !rc; i++)
+			rc = process_rx(w->xsks, i);
 		if (rc && !w->err)
 			w->err = rc;
 	}
+	// a batch still in flight is completed and routed (on a stop its tx frames
+	// go back to the fill rings: dispose sees the stop)
+	const int rc = finish_pending(w);
+	if (rc && !w->err)
+		w->err = rc;
 	return NULL;
 }
 
@@ -846,6 +917,8 @@ static void release_all(void)
 			free(wk->xsks);
 			free(wk->descs);
 			free(wk->verdicts);
+			free(wk->pend_descs);
+			free(wk->pend_verdicts);
 			free(wk->to_drop);
 			free(wk->to_tx);
 			free(wk->ntx);
@@ -892,13 +965,15 @@ static int init_worker(struct worker *w)
 	w->xsks = calloc(nif, sizeof(*w->xsks));
 	w->descs = calloc(b, sizeof(*w->descs));
 	w->verdicts = calloc(b, sizeof(*w->verdicts));
+	w->pend_descs = calloc(b, sizeof(*w->pend_descs));
+	w->pend_verdicts = calloc(b, sizeof(*w->pend_verdicts));
 	w->to_drop = calloc(b, sizeof(*w->to_drop));
 	w->to_tx = calloc(b * nif, sizeof(*w->to_tx));
 	w->ntx = calloc(nif, sizeof(*w->ntx));
 	w->to_fill = calloc(b * nif, sizeof(*w->to_fill));
 	w->nfill = calloc(nif, sizeof(*w->nfill));
-	if (!w->xsks || !w->descs || !w->verdicts || !w->to_drop || !w->to_tx || !w->ntx ||
-	    !w->to_fill || !w->nfill)
+	if (!w->xsks || !w->descs || !w->verdicts || !w->pend_descs || !w->pend_verdicts || !w->to_drop ||
+	    !w->to_tx || !w->ntx || !w->to_fill || !w->nfill)
 		return -ENOMEM;
 	for (unsigned i = 0; i < nif; i++)
 		w->xsks[i].fd = -1;
@@ -1010,7 +1085,7 @@ int xsknf_start_workers(void)
 {
 	if (!initialised)
 		return -EINVAL;
-	if (!batch_fn && !packet_fn && !xsknf_packet_processor)
+	if (!submit_fn && !batch_fn && !packet_fn && !xsknf_packet_processor)
 		return -ENOENT;   // no NF linked in and none registered
 	__atomic_store_n(&stop_flag, 0, __ATOMIC_RELAXED);
 	// worker i runs on the i-th CPU of the process's affinity set (src/xsknf.c:1049-1095)
@@ -1116,6 +1191,19 @@ int xsknf_set_packet_processor(xsknf_packet_processor_fn fn)
 int xsknf_set_batch_processor(xsknf_batch_processor_fn fn, void *user)
 {
 	batch_fn = fn;
+	batch_user = user;
+	submit_fn = NULL;
+	complete_fn = NULL;
+	return 0;
+}
+
+int xsknf_set_batch_processor_async(xsknf_batch_submit_fn submit, xsknf_batch_complete_fn complete, void *user)
+{
+	if (!submit != !complete)
+		return -EINVAL;
+	submit_fn = submit;
+	complete_fn = complete;
+	batch_fn = NULL;
 	batch_user = user;
 	return 0;
 }

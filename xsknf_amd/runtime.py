@@ -26,6 +26,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libx
 EXPORTED_SYMBOLS = (
     "xsknf_parse_args", "xsknf_init", "xsknf_cleanup", "xsknf_start_workers", "xsknf_stop_workers",
     "xsknf_get_socket_stats", "xsknf_set_packet_processor", "xsknf_set_batch_processor",
+    "xsknf_set_batch_processor_async",
     "xsknf_get_umem", "xsknf_worker_error", "xsknf_emu_deliver", "xsknf_emu_transmit",
 )
 
@@ -94,6 +95,7 @@ def load() -> ctypes.CDLL:
     lib.xsknf_get_socket_stats.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(SocketStats)]
     lib.xsknf_set_packet_processor.argtypes = [ctypes.c_void_p]
     lib.xsknf_set_batch_processor.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.xsknf_set_batch_processor_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.xsknf_get_umem.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(ctypes.c_void_p),
                                    ctypes.POINTER(ctypes.c_uint64)]
     lib.xsknf_worker_error.argtypes = [ctypes.c_uint]
@@ -169,6 +171,12 @@ class Runtime:
     def set_batch_processor(self, fn_ptr: Optional[int], user: Optional[int] = None) -> None:
         _check(self.lib.xsknf_set_batch_processor(ctypes.c_void_p(fn_ptr), ctypes.c_void_p(user)),
                "set_batch_processor")
+
+    def set_batch_processor_async(self, submit_ptr: int, complete_ptr: int, user: Optional[int] = None) -> None:
+        """The two-phase hook (xsknf_batch_submit_fn / xsknf_batch_complete_fn): one batch
+        in flight per worker while the next is received."""
+        _check(self.lib.xsknf_set_batch_processor_async(ctypes.c_void_p(submit_ptr), ctypes.c_void_p(complete_ptr),
+                                                        ctypes.c_void_p(user)), "set_batch_processor_async")
 
     # -- lifecycle ----------------------------------------------------------
     def start(self) -> None:
@@ -251,6 +259,14 @@ class GpuHook:
     @property
     def fn_ptr(self) -> int:
         return ctypes.cast(self.lib.xsknf_gpu_hook_process, ctypes.c_void_p).value
+
+    @property
+    def submit_ptr(self) -> int:
+        return ctypes.cast(self.lib.xsknf_gpu_hook_submit, ctypes.c_void_p).value
+
+    @property
+    def complete_ptr(self) -> int:
+        return ctypes.cast(self.lib.xsknf_gpu_hook_complete, ctypes.c_void_p).value
 
     def stats(self, worker: int = 0) -> dict:
         s = _lib.CtxStats()
