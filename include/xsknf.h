@@ -121,15 +121,22 @@ typedef int (*xsknf_batch_processor_fn)(void *user, unsigned worker_idx, void *u
 /* Two-phase batch hook: `submit` starts the NF on a batch as the one-call hook
  * would (same arguments) and returns at once with a ticket; `complete` blocks
  * until that batch's verdicts -- and any writes into its frames -- are done.
- * The worker keeps one batch in flight: it submits batch k+1, then completes
- * and routes batch k, so an accelerator's round trip overlaps the next rx.  A
- * batch in flight is completed without waiting for more traffic when the rx
- * ring runs dry, and before the worker stops.  The frames, descriptors and
+ * The worker keeps batches in flight (one by default, xsknf_set_batch_depth):
+ * it submits batch k+1, then completes and routes batch k, so an accelerator's
+ * round trip overlaps the next rx.  Batches in flight are completed without
+ * waiting for more traffic when the rx ring runs dry, and before the worker
+ * stops.  The frames, descriptors and
  * verdicts of a batch stay untouched by the runtime until its complete. */
 typedef int (*xsknf_batch_submit_fn)(void *user, unsigned worker_idx, void *umem,
 		uint64_t umem_size, const struct xdp_desc *descs, uint32_t n,
 		unsigned ingress_ifindex, int32_t *verdicts, uint64_t *ticket);
 typedef int (*xsknf_batch_complete_fn)(void *user, unsigned worker_idx, void *umem, uint64_t ticket);
+
+/* Batches a worker keeps in flight with the two-phase hook (1 .. XSKNF_MAX_HOOK_DEPTH,
+ * default 1): after submitting a batch it completes the oldest only while more
+ * than `depth` are out.  Call before xsknf_start_workers(). */
+#define XSKNF_MAX_HOOK_DEPTH 4
+XSKNF_API int xsknf_set_batch_depth(unsigned depth);
 
 /* Select the NF: call before xsknf_start_workers().  A batch hook (one-call or
  * two-phase; the last set wins) takes precedence; with neither set, the

@@ -62,6 +62,8 @@ def gpu():
 @pytest.mark.parametrize("lib_args,app_args,count,queues,tx", [
     # the harness's own invocation (DROP), 64 B frames
     (["-i", "emu0"], ["-q", "-i", "1", "-c", "DROP", "-G", "20000:64"], 20000, 1, False),
+    # four batches in flight
+    (["-i", "emu0", "-b", "32"], ["-q", "-d", "4", "-c", "REDIRECT", "-G", "9000:570"], 9000, 1, True),
     # REDIRECT (hairpin: the generator drains the tx ring), 1500 B, two workers, big batches
     (["-i", "emu0", "-w", "2", "-b", "256"], ["-q", "-c", "REDIRECT", "-G", "8000:1500"], 8000, 2, True),
     # the STAGED host path, several iterations
@@ -69,7 +71,7 @@ def gpu():
      False),
     # the one-call hook (one batch at a time) instead of the default two-phase one
     (["-i", "emu0"], ["-q", "-s", "-c", "DROP", "-G", "20000:64"], 20000, 1, False),
-], ids=["drop-64", "redirect-1500-w2", "staged-570", "drop-64-gpu-sync"])
+], ids=["drop-64", "redirect-570-depth4", "redirect-1500-w2", "staged-570", "drop-64-gpu-sync"])
 def test_stats_txt_on_sigusr1(gpu, clean_ctx, tmp_path, lib_args, app_args, count, queues, tx):
     want = count * queues
     with clean_ctx.Pool(1) as pool:

@@ -23,13 +23,14 @@ def frames():
     return config1.frames_check(9000)
 
 
-def run_loop(cfg, plan, n_if=1, two_phase=False, **hook_kw):
+def run_loop(cfg, plan, n_if=1, two_phase=False, depth=1, **hook_kw):
     hook = R.GpuHook(workers=cfg.workers, max_batch=cfg.batch_size, num_interfaces=n_if,
                      frame_len_hint=cfg.xsk_frame_size, **hook_kw)
     rt = R.Runtime(cfg)
     try:
         if two_phase:   # xsknf_gpu_hook_submit / _complete: one batch in flight per worker
             rt.set_batch_processor_async(hook.submit_ptr, hook.complete_ptr, hook.handle)
+            rt.set_batch_depth(depth)
         else:
             rt.set_batch_processor(hook.fn_ptr, hook.handle)
         rt.start()
@@ -54,6 +55,17 @@ def test_gpu_hook_redirect_matches_oracle(frames, path, batch, two_phase):
     assert got[0] == want
     assert hs["frames"] == len(frames) == st[0]["rx_npkts"]
     assert hs["batches"] >= len(frames) // batch
+
+
+@pytest.mark.parametrize("path", [_lib.PATH_ZEROCOPY, _lib.PATH_STAGED], ids=["zerocopy", "staged"])
+@pytest.mark.parametrize("depth", [2, 4])
+def test_gpu_hook_batches_in_flight(frames, path, depth):
+    """Two-phase hook with up to `depth` batches out per worker (the context has
+    4 slots: a 5th submit completes the oldest itself)."""
+    cfg = R.make_config(["emu0"], batch_size=64)
+    got, hs, st = run_loop(cfg, {0: frames}, two_phase=True, depth=depth, path=path, iterations=3)
+    assert got[0] == [b for v, b in expected(frames, iterations=3) if v != -1]
+    assert hs["frames"] == len(frames) == st[0]["rx_npkts"]
 
 
 def test_gpu_hook_drop(frames):

@@ -200,12 +200,13 @@ def async_stats(worker=0):
     return sub.value, ovl.value
 
 
-@pytest.mark.parametrize("batch", [1, 64, 2048])
-def test_async_hook_round_trip(frames, batch):
+@pytest.mark.parametrize("batch,depth", [(1, 1), (64, 1), (2048, 1), (64, 3), (7, 4)])
+def test_async_hook_round_trip(frames, batch, depth):
     """Two-phase hook: batch k is routed only after its complete, while batch k+1
-    is in flight; output identical to the per-frame path, in order."""
+    (.. k+depth) is in flight; output identical to the per-frame path, in order."""
     with R.Runtime(R.make_config(["emu0"], batch_size=batch)) as rt:
         rt.set_batch_processor_async(*nf_oracle_async(iterations=2))
+        rt.set_batch_depth(depth)
         rt.start()
         got = pump(rt, {0: frames})[0]
         st = rt.stats()
@@ -257,6 +258,9 @@ def test_async_hook_stop_and_restart_loses_no_frame(frames):
 
 def test_init_and_start_errors():
     lib = R.load()
+    assert lib.xsknf_set_batch_depth(0) == -errno.EINVAL
+    assert lib.xsknf_set_batch_depth(5) == -errno.EINVAL
+    assert lib.xsknf_set_batch_processor_async(ctypes.c_void_p(1), None, None) == -errno.EINVAL
     cfg = R.make_config(["emu0"])
     cfg.working_mode = R.MODE_XDP
     assert lib.xsknf_init(ctypes.byref(cfg), None) == -errno.EOPNOTSUPP

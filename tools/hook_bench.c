@@ -11,7 +11,7 @@
 // Eth/IPv4/UDP frames and drains the tx ring, and counts what the worker
 // received over SECONDS after a half-second warm-up.
 //
-//   hook_bench MODE LEN BATCH SECONDS [ZEROCOPY|STAGED]
+//   hook_bench MODE LEN BATCH SECONDS [ZEROCOPY|STAGED [DEPTH]]   (DEPTH: batches in flight, async)
 //
 // Prints one JSON line.  Tool, not product: it links the oracle only as the CPU
 // NF of mode "cpu" (the reference path, as tools/config1.py does).
@@ -60,6 +60,7 @@ int main(int argc, char **argv)
 	const unsigned batch = (unsigned)atoi(argv[3]);
 	const double secs = atof(argv[4]);
 	const int path = argc > 5 && !strcmp(argv[5], "STAGED") ? XSKNF_GPU_PATH_STAGED : XSKNF_GPU_PATH_ZEROCOPY;
+	const unsigned depth = argc > 6 ? (unsigned)atoi(argv[6]) : 1;
 	if (len < 42 || len > 3800 || batch == 0) {
 		fprintf(stderr, "bad LEN / BATCH\n");
 		return 2;
@@ -99,6 +100,10 @@ int main(int argc, char **argv)
 		else
 			xsknf_set_batch_processor_async((xsknf_batch_submit_fn)xsknf_gpu_hook_submit,
 					(xsknf_batch_complete_fn)xsknf_gpu_hook_complete, hook);
+		if (xsknf_set_batch_depth(depth)) {
+			fprintf(stderr, "bad DEPTH\n");
+			return 2;
+		}
 	}
 
 	// frames as tests/gen-traffic.lua builds them (Eth/IPv4 ihl 5/UDP, 256 flows)
@@ -155,9 +160,9 @@ int main(int argc, char **argv)
 		xsknf_gpu_hook_destroy(hook);
 	xsknf_cleanup();
 	const double mpps = rx / (t1 - tm) / 1e6;
-	printf("{\"mode\": \"%s\", \"len\": %u, \"batch\": %u, \"path\": \"%s\", \"seconds\": %.2f, "
-	       "\"mpps\": %.3f, \"gbps\": %.2f, \"worker_error\": %d}\n",
-	       mode, len, batch, path == XSKNF_GPU_PATH_STAGED ? "STAGED" : "ZEROCOPY", t1 - tm, mpps,
+	printf("{\"mode\": \"%s\", \"len\": %u, \"batch\": %u, \"path\": \"%s\", \"depth\": %u, "
+	       "\"seconds\": %.2f, \"mpps\": %.3f, \"gbps\": %.2f, \"worker_error\": %d}\n",
+	       mode, len, batch, path == XSKNF_GPU_PATH_STAGED ? "STAGED" : "ZEROCOPY", depth, t1 - tm, mpps,
 	       mpps * len / 1e3, err);
 	free(frames);
 	free(txbuf);

@@ -39,6 +39,7 @@ static int opt_csum_iterations = 1;
 static int opt_quiet, opt_extra_stats, opt_app_stats;
 static int opt_gpu_path = XSKNF_GPU_PATH_ZEROCOPY;
 static int opt_gpu_sync;
+static int opt_gpu_depth;   // 0: by batch size
 static unsigned long opt_gen_count;
 static unsigned opt_gen_len = 64;
 static volatile sig_atomic_t benchmark_done, stats_requested;
@@ -52,6 +53,7 @@ static const struct option long_options[] = {
 	{"app-stats", no_argument, 0, 'a'},
 	{"gpu-path", required_argument, 0, 'g'},
 	{"gpu-sync", no_argument, 0, 's'},
+	{"gpu-depth", required_argument, 0, 'd'},
 	{"emu-gen", required_argument, 0, 'G'},
 	{0, 0, 0, 0},
 };
@@ -69,6 +71,8 @@ static void usage(const char *prog)
 		"  -g, --gpu-path	ZEROCOPY (default) or STAGED host path to the GPU.\n"
 		"  -s, --gpu-sync	One batch at a time (default: the next batch is received\n"
 		"			while the GPU checksums the last one).\n"
+		"  -d, --gpu-depth	Batches in flight per worker, 1-4 (default 2 for batches\n"
+		"			of up to 128 frames, else 1).\n"
 		"  -G, --emu-gen		COUNT[:LEN] frames per emulated queue from a built-in generator.\n"
 		"\n",
 		prog);
@@ -78,7 +82,7 @@ static void usage(const char *prog)
 static void parse_command_line(int argc, char **argv, char *app_path)
 {
 	int option_index, c;
-	while ((c = getopt_long(argc, argv, "qxasi:c:g:G:", long_options, &option_index)) != -1) {
+	while ((c = getopt_long(argc, argv, "qxasd:i:c:g:G:", long_options, &option_index)) != -1) {
 		switch (c) {
 		case 'c':
 			if (!strcmp(optarg, "REDIRECT")) {
@@ -104,6 +108,13 @@ static void parse_command_line(int argc, char **argv, char *app_path)
 			break;
 		case 's':
 			opt_gpu_sync = 1;
+			break;
+		case 'd':
+			opt_gpu_depth = atoi(optarg);
+			if (opt_gpu_depth < 1 || opt_gpu_depth > XSKNF_MAX_HOOK_DEPTH) {
+				fprintf(stderr, "ERROR: invalid gpu depth %s\n", optarg);
+				usage(basename(app_path));
+			}
 			break;
 		case 'g':
 			if (!strcmp(optarg, "ZEROCOPY")) {
@@ -342,6 +353,9 @@ int main(int argc, char **argv)
 	else
 		xsknf_set_batch_processor_async((xsknf_batch_submit_fn)xsknf_gpu_hook_submit,
 				(xsknf_batch_complete_fn)xsknf_gpu_hook_complete, hook);
+	// two in flight pay at the reference's small batches, not from 256 frames on
+	// (tools/hook_bench.c: 1500 B x 64 5.8 -> 8.2 Mpps, x 256 13.2 -> 11.8)
+	xsknf_set_batch_depth(opt_gpu_depth ? (unsigned)opt_gpu_depth : (config.batch_size <= 128 ? 2u : 1u));
 	rc = xsknf_start_workers();
 	if (rc) {
 		fprintf(stderr, "ERROR: xsknf_start_workers: %s\n", strerror(-rc));

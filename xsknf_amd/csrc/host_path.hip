@@ -50,7 +50,7 @@
 
 namespace {
 
-constexpr int kSlots = 2;
+constexpr int kSlots = 4;   // pieces in flight per context (the runtime keeps up to 3 batches out)
 constexpr uint32_t kPiece = 65536;          // frames per slot submission of process_batch
 constexpr uint64_t kMergeGap = 256;         // frames closer than this share one DMA run
 constexpr size_t kMaxDmaRuns = 8;           // more runs than this (and no 2-D shape): mapped reads

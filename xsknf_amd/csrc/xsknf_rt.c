@@ -96,6 +96,8 @@ struct xsk_sock {
 	unsigned long emu_rx_full, emu_fill_empty;
 };
 
+#define PEND_RING (XSKNF_MAX_HOOK_DEPTH + 1)
+
 struct worker {
 	unsigned id;
 	pthread_t thread;
@@ -108,13 +110,18 @@ struct worker {
 	// per-batch scratch, sized by batch_size at init
 	struct xdp_desc *descs;
 	int32_t *verdicts;
-	// two-phase hook: the batch in flight (its own descriptor / verdict arrays;
-	// descs / verdicts above take the next one, and the two swap)
-	struct xdp_desc *pend_descs;
-	int32_t *pend_verdicts;
-	uint32_t pend_n;                     // 0: none in flight
-	unsigned pend_if;                    // the rx interface it came from
-	uint64_t pend_ticket;
+	// two-phase hook: the batches in flight, oldest first, a ring of PEND_RING
+	// (up to depth + 1 between a submit and the completion it triggers; each
+	// with its own descriptor / verdict arrays, which swap with descs /
+	// verdicts above when a batch is submitted)
+	struct pending {
+		struct xdp_desc *descs;
+		int32_t *verdicts;
+		uint32_t n;
+		unsigned ifindex;            // the rx interface it came from
+		uint64_t ticket;
+	} pend[PEND_RING];
+	unsigned pend_head, pend_count;
 	struct pkt_info *to_drop;
 	struct pkt_info *to_tx;              // [num_interfaces][batch_size]
 	uint32_t *ntx;
@@ -149,6 +156,7 @@ static xsknf_batch_processor_fn batch_fn;
 static void *batch_user;
 static xsknf_batch_submit_fn submit_fn;
 static xsknf_batch_complete_fn complete_fn;
+static unsigned hook_depth = 1;          // batches a worker keeps in flight (two-phase hook)
 
 static inline uint64_t addr_offset(uint64_t addr)
 {
@@ -662,24 +670,36 @@ static int dispose(struct xsk_sock *xsks, unsigned ifindex, const struct xdp_des
 				       : dispose_1if(&xsks[ifindex], descs, verdicts, n);
 }
 
-// The batch in flight (two-phase hook): wait for its verdicts, then route it.
-static int finish_pending(struct worker *w)
+// The oldest batch in flight (two-phase hook): wait for its verdicts, then route it.
+static int finish_oldest(struct worker *w)
 {
-	if (!w->pend_n)
+	if (!w->pend_count)
 		return 0;
-	struct xsk_sock *rx = &w->xsks[w->pend_if];
-	const uint32_t n = w->pend_n;
-	w->pend_n = 0;
-	int rc = complete_fn(batch_user, w->id, rx->buffer, w->pend_ticket);
+	struct pending *b = &w->pend[w->pend_head];
+	w->pend_head = (w->pend_head + 1) % PEND_RING;
+	w->pend_count--;
+	struct xsk_sock *rx = &w->xsks[b->ifindex];
+	int rc = complete_fn(batch_user, w->id, rx->buffer, b->ticket);
 	if (rc) {
 		// verdicts unknown: the frames go back to the rx socket's fill ring
 		struct pkt_info *p = w->to_drop;
-		for (uint32_t i = 0; i < n; i++)
-			p[i] = (struct pkt_info){w->pend_descs[i].addr, w->pend_descs[i].len};
-		recycle_pkts(rx, p, n);
+		for (uint32_t i = 0; i < b->n; i++)
+			p[i] = (struct pkt_info){b->descs[i].addr, b->descs[i].len};
+		recycle_pkts(rx, p, b->n);
 		return rc;
 	}
-	return dispose(w->xsks, w->pend_if, w->pend_descs, w->pend_verdicts, n);
+	return dispose(w->xsks, b->ifindex, b->descs, b->verdicts, b->n);
+}
+
+static int finish_all(struct worker *w)
+{
+	int rc = 0;
+	while (w->pend_count) {
+		const int r = finish_oldest(w);
+		if (r && !rc)
+			rc = r;
+	}
+	return rc;
 }
 
 // One rx batch of interface ifindex (process_batch_1if / process_batch,
@@ -696,8 +716,8 @@ static int process_rx(struct xsk_sock *xsks, unsigned ifindex)
 	uint32_t idx;
 	const uint32_t rcvd = ring_peek(&rx->rx, conf.batch_size, &idx);
 	if (!rcvd) {
-		// nothing new: the batch in flight is not held back waiting for traffic
-		if ((rc = finish_pending(w)))
+		// nothing new: the batches in flight are not held back waiting for traffic
+		if ((rc = finish_all(w)))
 			return rc;
 		rx_empty(rx);
 		return 0;
@@ -718,18 +738,16 @@ static int process_rx(struct xsk_sock *xsks, unsigned ifindex)
 		recycle_pkts(rx, p, rcvd);
 		return rc;
 	}
-	rc = finish_pending(w);
-	// the new batch becomes the one in flight; its arrays swap with the scratch
-	struct xdp_desc *d = w->pend_descs;
-	int32_t *v = w->pend_verdicts;
-	w->pend_descs = w->descs;
-	w->pend_verdicts = w->verdicts;
+	// the new batch joins the ones in flight; its arrays swap with a free slot's
+	struct pending *b = &w->pend[(w->pend_head + w->pend_count) % PEND_RING];
+	struct xdp_desc *d = b->descs;
+	int32_t *v = b->verdicts;
+	*b = (struct pending){w->descs, w->verdicts, rcvd, ifindex, ticket};
 	w->descs = d;
 	w->verdicts = v;
-	w->pend_n = rcvd;
-	w->pend_if = ifindex;
-	w->pend_ticket = ticket;
-	return rc;
+	w->pend_count++;
+	// then the oldest is completed and routed once more than hook_depth are out
+	return w->pend_count > hook_depth ? finish_oldest(w) : 0;
 }
 
 // worker_loop (src/xsknf.c:716-742)
@@ -760,7 +778,7 @@ static void *worker_loop(void *arg)
 	}
 	// a batch still in flight is completed and routed (on a stop its tx frames
 	// go back to the fill rings: dispose sees the stop)
-	const int rc = finish_pending(w);
+	const int rc = finish_all(w);
 	if (rc && !w->err)
 		w->err = rc;
 	return NULL;
@@ -917,8 +935,10 @@ static void release_all(void)
 			free(wk->xsks);
 			free(wk->descs);
 			free(wk->verdicts);
-			free(wk->pend_descs);
-			free(wk->pend_verdicts);
+			for (unsigned k = 0; k < PEND_RING; k++) {
+				free(wk->pend[k].descs);
+				free(wk->pend[k].verdicts);
+			}
 			free(wk->to_drop);
 			free(wk->to_tx);
 			free(wk->ntx);
@@ -965,15 +985,19 @@ static int init_worker(struct worker *w)
 	w->xsks = calloc(nif, sizeof(*w->xsks));
 	w->descs = calloc(b, sizeof(*w->descs));
 	w->verdicts = calloc(b, sizeof(*w->verdicts));
-	w->pend_descs = calloc(b, sizeof(*w->pend_descs));
-	w->pend_verdicts = calloc(b, sizeof(*w->pend_verdicts));
+	int pend_ok = 1;
+	for (unsigned k = 0; k < PEND_RING; k++) {
+		w->pend[k].descs = calloc(b, sizeof(*w->pend[k].descs));
+		w->pend[k].verdicts = calloc(b, sizeof(*w->pend[k].verdicts));
+		pend_ok &= w->pend[k].descs && w->pend[k].verdicts;
+	}
 	w->to_drop = calloc(b, sizeof(*w->to_drop));
 	w->to_tx = calloc(b * nif, sizeof(*w->to_tx));
 	w->ntx = calloc(nif, sizeof(*w->ntx));
 	w->to_fill = calloc(b * nif, sizeof(*w->to_fill));
 	w->nfill = calloc(nif, sizeof(*w->nfill));
-	if (!w->xsks || !w->descs || !w->verdicts || !w->pend_descs || !w->pend_verdicts || !w->to_drop ||
-	    !w->to_tx || !w->ntx || !w->to_fill || !w->nfill)
+	if (!w->xsks || !w->descs || !w->verdicts || !pend_ok || !w->to_drop || !w->to_tx || !w->ntx ||
+	    !w->to_fill || !w->nfill)
 		return -ENOMEM;
 	for (unsigned i = 0; i < nif; i++)
 		w->xsks[i].fd = -1;
@@ -1194,6 +1218,14 @@ int xsknf_set_batch_processor(xsknf_batch_processor_fn fn, void *user)
 	batch_user = user;
 	submit_fn = NULL;
 	complete_fn = NULL;
+	return 0;
+}
+
+int xsknf_set_batch_depth(unsigned depth)
+{
+	if (depth < 1 || depth > XSKNF_MAX_HOOK_DEPTH)
+		return -EINVAL;
+	hook_depth = depth;
 	return 0;
 }
 

@@ -26,7 +26,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libx
 EXPORTED_SYMBOLS = (
     "xsknf_parse_args", "xsknf_init", "xsknf_cleanup", "xsknf_start_workers", "xsknf_stop_workers",
     "xsknf_get_socket_stats", "xsknf_set_packet_processor", "xsknf_set_batch_processor",
-    "xsknf_set_batch_processor_async",
+    "xsknf_set_batch_processor_async", "xsknf_set_batch_depth",
     "xsknf_get_umem", "xsknf_worker_error", "xsknf_emu_deliver", "xsknf_emu_transmit",
 )
 
@@ -96,6 +96,7 @@ def load() -> ctypes.CDLL:
     lib.xsknf_set_packet_processor.argtypes = [ctypes.c_void_p]
     lib.xsknf_set_batch_processor.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     lib.xsknf_set_batch_processor_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.xsknf_set_batch_depth.argtypes = [ctypes.c_uint]
     lib.xsknf_get_umem.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(ctypes.c_void_p),
                                    ctypes.POINTER(ctypes.c_uint64)]
     lib.xsknf_worker_error.argtypes = [ctypes.c_uint]
@@ -178,6 +179,9 @@ class Runtime:
         _check(self.lib.xsknf_set_batch_processor_async(ctypes.c_void_p(submit_ptr), ctypes.c_void_p(complete_ptr),
                                                         ctypes.c_void_p(user)), "set_batch_processor_async")
 
+    def set_batch_depth(self, depth: int) -> None:
+        _check(self.lib.xsknf_set_batch_depth(depth), "set_batch_depth")
+
     # -- lifecycle ----------------------------------------------------------
     def start(self) -> None:
         _check(self.lib.xsknf_start_workers(), "xsknf_start_workers")
@@ -194,6 +198,7 @@ class Runtime:
         # clear the NF so a later Runtime does not inherit it
         self.lib.xsknf_set_batch_processor(None, None)
         self.lib.xsknf_set_packet_processor(None)
+        self.lib.xsknf_set_batch_depth(1)
         return rc
 
     def __enter__(self):
