@@ -170,7 +170,7 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            the 4-byte records come back and the host writes
  *                            the 2 check bytes.  A batch of frames scattered
  *                            over the UMEM runs as ZEROCOPY instead.
- * One context = one worker thread.  It keeps two batches in flight (two slots,
+ * One context = one worker thread.  It keeps up to four batches in flight (four slots,
  * each with its own HIP stream): the copies and kernel of one overlap the
  * other's, and the host's share of one overlaps the device's share of the other.
  * xsknf_gpu_ctx_process_batch() is synchronous: when it returns, verdicts and

@@ -205,7 +205,7 @@ class HostPath:
         return verdicts
 
     def submit(self, descs, verdicts, ingress_ifindex: int = 0) -> int:
-        """Enqueue a batch (two in flight per context); returns its ticket.  The
+        """Enqueue a batch (up to four in flight per context); returns its ticket.  The
         verdicts array and the batch's frames belong to the context until
         wait(ticket)."""
         if descs.dtype.itemsize != 16 or not descs.flags.c_contiguous:

@@ -13,7 +13,7 @@
 // (copy plan, writing the checks) overlaps the device's share of the
 // other.  xsknf_gpu_ctx_submit() / _wait() expose the pipeline; the
 // synchronous xsknf_gpu_ctx_process_batch() cuts a large batch into pieces of
-// kPiece frames and runs them through the same two slots.
+// kPiece frames and runs them through the same slots.
 //
 // ZEROCOPY: the UMEM is pinned and mapped into the device address space; the
 //   kernel reads the frames and writes the check bytes over PCIe, in place.
@@ -33,7 +33,7 @@
 //   reads with host-applied checks 23 GB/s, host-bound; in place 41 GB/s).
 //   Copying frames back would overwrite frames outside the batch that the
 //   kernel / NIC may be filling concurrently (fill-ring frames), so it never
-//   does; the mirror is only read by the kernels, so two batches in flight may
+//   does; the mirror is only read by the kernels, so batches in flight may
 //   share it (their frames are distinct, and a run's gap bytes are the host's
 //   own bytes).
 #include <hip/hip_runtime.h>
