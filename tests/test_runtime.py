@@ -345,3 +345,15 @@ def test_veth_config1_is_bit_exact():
     assert res["exit"] == 0, res
     assert res["worker_error"] == 0
     assert res["expected"] > 1300 and res["mismatches"] == 0, res
+
+
+@pytest.mark.parametrize("extra", [("--two-phase",), ("--two-phase", "--poll"), ("--poll",)],
+                         ids=["two-phase", "two-phase-poll", "poll"])
+def test_veth_config1_hooks_and_poll(extra):
+    """Real AF_XDP sockets: the two-phase hook keeps a batch in flight across worker
+    passes, and with poll() a pass never blocks while one is out (the last batch
+    still comes back)."""
+    res = config1.check(iterations=1, n=1200, extra=extra)
+    assert res["exit"] == 0, res
+    assert res["worker_error"] == 0
+    assert res["expected"] > 1000 and res["mismatches"] == 0, res

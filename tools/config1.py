@@ -111,12 +111,13 @@ def run(args: list[str], timeout: float) -> dict:
     return res
 
 
-def check(iterations: int = 1, n: int = 3000) -> dict:
+def check(iterations: int = 1, n: int = 3000, extra: tuple = ()) -> dict:
+    """extra: more harness flags (--two-phase, --poll, --batch B)."""
     sent = frames_check(n)
     with tempfile.TemporaryDirectory() as d:
         fin, fout = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
         write_frames(fin, sent)
-        res = run(["--frames", fin, "--check", fout, "--iterations", str(iterations)], 120)
+        res = run(["--frames", fin, "--check", fout, "--iterations", str(iterations), *extra], 120)
         if res.get("exit") != 0:
             return res
         back = [f for f in read_frames(fout) if f[6:12] == SRC_MAC]

@@ -48,6 +48,9 @@
 // the oracle's reference-shaped callback (oracle/csum_oracle.c)
 void oracle_nf_set_options(int32_t csum_iterations, int32_t action, uint32_t num_interfaces);
 int oracle_nf_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex);
+int oracle_nf_batch_submit(void *user, unsigned worker, void *umem, uint64_t umem_size,
+		const struct xdp_desc *descs, uint32_t n, unsigned ingress, int32_t *verdicts, uint64_t *ticket);
+int oracle_nf_batch_complete(void *user, unsigned worker, void *umem, uint64_t ticket);
 
 struct frames {
 	uint32_t n;
@@ -273,7 +276,7 @@ static int capture(const char *out_path, double secs, unsigned long *got)
 int main(int argc, char **argv)
 {
 	const char *frames_path = NULL, *check_out = NULL;
-	int iterations = 1, action_drop = 1, search = 0, nf_cpu = 0, batch = 64;
+	int iterations = 1, action_drop = 1, search = 0, nf_cpu = 0, batch = 64, two_phase = 0, use_poll = 0;
 	double max_mpps = 4.0, step_mpps = 0.05, trial_s = 2.0;
 	for (int i = 1; i < argc; i++) {
 		const char *a = argv[i];
@@ -288,10 +291,12 @@ int main(int argc, char **argv)
 		else if (!strcmp(a, "--trial-s") && v) { trial_s = atof(v); i++; }
 		else if (!strcmp(a, "--generators") && v) { gen_threads = atoi(v); i++; }
 		else if (!strcmp(a, "--batch") && v) { batch = atoi(v); i++; }
+		else if (!strcmp(a, "--two-phase")) { two_phase = 1; }
+		else if (!strcmp(a, "--poll")) { use_poll = 1; }
 		else {
 			fprintf(stderr, "usage: %s --frames F [--search|--check OUT] [--iterations k] "
 				"[--redirect] [--max-mpps M] [--step-mpps S] [--trial-s T] [--generators G] "
-				"[--batch B]\n", argv[0]);
+				"[--batch B] [--two-phase] [--poll]\n", argv[0]);
 			return 2;
 		}
 	}
@@ -329,8 +334,12 @@ int main(int argc, char **argv)
 	cfg.xdp_flags = XDP_FLAGS_UPDATE_IF_NOEXIST | XDP_FLAGS_SKB_MODE;
 	cfg.batch_size = (uint32_t)batch;
 	cfg.xsk_frame_size = 4096;
+	cfg.poll = use_poll;
 	oracle_nf_set_options(iterations, action_drop, 1);
-	xsknf_set_packet_processor(oracle_nf_packet_processor);
+	if (two_phase)   // the NF as a two-phase batch hook: batches in flight across worker passes
+		xsknf_set_batch_processor_async(oracle_nf_batch_submit, oracle_nf_batch_complete, NULL);
+	else
+		xsknf_set_packet_processor(oracle_nf_packet_processor);
 	// worker on the first CPU of our set, generators on the next ones
 	cpu_set_t set;
 	pthread_getaffinity_np(pthread_self(), sizeof(set), &set);

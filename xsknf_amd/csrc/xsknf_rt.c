@@ -704,9 +704,9 @@ static int finish_all(struct worker *w)
 
 // One rx batch of interface ifindex (process_batch_1if / process_batch,
 // src/xsknf.c:630-714, :478-585).  With the two-phase hook the batch is
-// submitted, and the previous one -- submitted on the last call -- is
-// completed and routed while this one runs.
-static int process_rx(struct xsk_sock *xsks, unsigned ifindex)
+// submitted, and the oldest in flight is completed and routed once more than
+// hook_depth are out.  *rcvd_any is set when a batch came in.
+static int process_rx(struct xsk_sock *xsks, unsigned ifindex, int *rcvd_any)
 {
 	struct xsk_sock *rx = &xsks[ifindex];
 	struct worker *w = rx->worker;
@@ -716,12 +716,10 @@ static int process_rx(struct xsk_sock *xsks, unsigned ifindex)
 	uint32_t idx;
 	const uint32_t rcvd = ring_peek(&rx->rx, conf.batch_size, &idx);
 	if (!rcvd) {
-		// nothing new: the batches in flight are not held back waiting for traffic
-		if ((rc = finish_all(w)))
-			return rc;
 		rx_empty(rx);
 		return 0;
 	}
+	*rcvd_any = 1;
 	take_rx(rx, idx, rcvd);
 	if (!submit_fn) {
 		if ((rc = run_nf(rx, rcvd, ifindex)))
@@ -767,12 +765,17 @@ static void *worker_loop(void *arg)
 				fds[nfds].revents = 0;
 				nfds++;
 			}
-			if (nfds && poll(fds, nfds, POLL_TIMEOUT_MS) <= 0)
+			// (batches in flight: no blocking poll, they are flushed below)
+			if (nfds && poll(fds, nfds, w->pend_count ? 0 : POLL_TIMEOUT_MS) <= 0 && !w->pend_count)
 				continue;
 		}
-		int rc = 0;
+		int rc = 0, rcvd_any = 0;
 		for (unsigned i = 0; i < conf.num_interfaces && !rc; i++)
-			rc = process_rx(w->xsks, i);
+			rc = process_rx(w->xsks, i, &rcvd_any);
+		// a pass with no traffic on any interface: the batches in flight are
+		// completed and routed, not held back waiting for more
+		if (!rc && !rcvd_any)
+			rc = finish_all(w);
 		if (rc && !w->err)
 			w->err = rc;
 	}
