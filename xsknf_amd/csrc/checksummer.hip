@@ -971,12 +971,8 @@ struct ItemStageDMA {
 #endif
 constexpr int kTailTiles = XSKNF_TAIL_TILES;   // tiles whose patches are in flight together
 
-#ifndef XSKNF_TAIL_PRIO   // A/B: wave priority while patching (0: unchanged)
-#define XSKNF_TAIL_PRIO 0
-#endif
 __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t tile0, uint32_t waves, int lane) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (XSKNF_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(XSKNF_TAIL_PRIO);
   const int piece = lane & 3;
   constexpr int T = kTailTiles;
   for (uint32_t tb = tile0; tb * kWave < args.n; tb += T * waves) {
