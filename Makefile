@@ -40,7 +40,8 @@ VETH := tools/build/xsk_veth
 PROBE := tools/build/hbm_probe
 PROBELIB := tools/build/libhbm_probe.so
 HOOKBENCH := tools/build/hook_bench
-tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH)
+CTXLAT := tools/build/ctx_latency
+tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH) $(CTXLAT)
 $(PROBE): tools/hbm_probe.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Wno-inline-asm -o $@ $<
@@ -59,6 +60,11 @@ $(HOOKBENCH): tools/hook_bench.c $(RTLIB) $(LIB) oracle
 	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ tools/hook_bench.c \
 		-L$(LIBDIR) -lxsknf -lxsknf_gpu -Loracle/build -lcsum_oracle \
 		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread
+
+$(CTXLAT): tools/ctx_latency.c $(LIB)
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ $< -L$(LIBDIR) -lxsknf_gpu \
+		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 # A/B build: every kernel family and launch shape (tools/tune.py, tools/ab_libs.sh;
 # XSKNF_GPU_LIB=build/ab/libxsknf_gpu.so selects it).  Not the product.
