@@ -1042,6 +1042,92 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
   }
 }
 
+// The patch list: where the default shape (W = 8, two items in flight: 157
+// VGPRs, 3 waves per SIMD, so 3 blocks per CU) has LDS to spare, a deferred
+// check is not parked in `verdicts` but kept in the wave's LDS list, one
+// 8-byte entry per frame for its first kPatchTiles tiles: the check's 64-byte
+// sector as an index from the 64-byte-aligned UMEM base, and {valid, whole
+// sector, byte of the check in the sector, the check}.  The frame's final
+// verdict is stored in the tile's one verdict store, and the wave's patches
+// read neither records nor descriptors back: one round trip (the sectors)
+// instead of three.  Tiles past kPatchTiles (a wave with more tiles than that:
+// grids smaller than residency) take the record path (tail_scatter).
+#ifndef XSKNF_PATCH_TILES
+#define XSKNF_PATCH_TILES 6
+#endif
+#ifndef XSKNF_PATCH_T
+#define XSKNF_PATCH_T 2
+#endif
+constexpr int kPatchTiles = XSKNF_PATCH_TILES;   // 6 x 64 x 8 B x 4 waves = 12 KiB per block
+constexpr int kPatchT = XSKNF_PATCH_T;           // tiles whose sectors are in flight together
+constexpr uint32_t kPatchValid = 1u << 23, kPatchWhole = 1u << 22;
+constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with margin)
+
+__device__ __forceinline__ uint2 patch_entry(const KernelArgs &a, const FrameRef &r, int u, uint16_t c) {
+  const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
+  const uintptr_t ck = f0 + static_cast<uintptr_t>(u) + 6;
+  const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
+  const uintptr_t base = reinterpret_cast<uintptr_t>(a.umem) & ~static_cast<uintptr_t>(63);
+  const bool whole = sec >= f0 && sec + 64 <= f0 + static_cast<uintptr_t>(r.len) && (ck & 63) != 63;
+  return make_uint2(static_cast<uint32_t>((sec - base) >> 6),
+                    kPatchValid | (whole ? kPatchWhole : 0u) | static_cast<uint32_t>((ck & 63) << 16) | c);
+}
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void lds_store_u64(uint32_t a, uint2 v) {
+  const u32x2 x = {v.x, v.y};
+  *reinterpret_cast<__attribute__((address_space(3))) u32x2 *>(static_cast<uintptr_t>(a)) = x;
+}
+
+__device__ __forceinline__ uint2 lds_u64(uint32_t a) {
+  const u32x2 x = *reinterpret_cast<const __attribute__((address_space(3))) u32x2 *>(static_cast<uintptr_t>(a));
+  return make_uint2(x.x, x.y);
+}
+
+// The wave's patch list (ntiles tiles of 64 entries at LDS `pl`): 16 frames per
+// round, 4 lanes per frame, each frame's sector read and rewritten whole (one
+// non-temporal 64-byte store of 4 lanes), or its 2 check bytes where the sector
+// leaves the frame.  kPatchT tiles' sectors are in flight together.
+__device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t pl, int ntiles, int lane) {
+  const int piece = lane & 3;
+  uint8_t *const base = args.umem - (reinterpret_cast<uintptr_t>(args.umem) & 63);   // keeps global addressing
+  constexpr int T = kPatchT;
+  for (int t0 = 0; t0 < ntiles; t0 += T) {
+    uint4 v[T][4];
+    uint8_t *mine[T][4];
+    uint32_t info[T][4];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint2 e = t0 + t < ntiles ? lds_u64(pl + 8 * ((t0 + t) * kWave + 16 * k + (lane >> 2))) : make_uint2(0, 0);
+        info[t][k] = e.y;
+        uint8_t *sec = base + (static_cast<uint64_t>(e.x) << 6);
+        const bool whole = (e.y & (kPatchValid | kPatchWhole)) == (kPatchValid | kPatchWhole);
+        mine[t][k] = whole ? sec + 16 * piece : sec + ((e.y >> 16) & 63);
+        if (whole) v[t][k] = load_nt(reinterpret_cast<const uint4 *>(mine[t][k]));
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t c = info[t][k] & 0xffffu;
+        if ((info[t][k] & (kPatchValid | kPatchWhole)) == (kPatchValid | kPatchWhole)) {
+          const int o = static_cast<int>((info[t][k] >> 16) & 63) - 16 * piece;
+          uint4 w = put_byte(v[t][k], o, c);
+          w = put_byte(w, o + 1, c >> 8);
+          store_nt16(mine[t][k], w);
+        } else if ((info[t][k] & kPatchValid) && piece == 0) {
+          mine[t][k][0] = static_cast<uint8_t>(c);
+          mine[t][k][1] = static_cast<uint8_t>(c >> 8);
+        }
+      }
+    }
+  }
+}
+
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
 // +8-11 % from 2 -> 3 waves per SIMD, so the register budget is pinned.
@@ -1062,6 +1148,8 @@ void checksum_kernel_split(const KernelArgs args) {
   __shared__ __attribute__((aligned(16))) uint16_t itemq[kWavesPerBlock][kItemCap];
   __shared__ __attribute__((aligned(16))) uint4 meta[kWavesPerBlock][kWave];
   __shared__ __attribute__((aligned(16))) uint32_t accb[kWavesPerBlock][kWave];
+  constexpr int PT = (W == 8 && U == 2 && !DMA && !PFW) ? kPatchTiles : 0;   // patch list tiles
+  __shared__ __attribute__((aligned(16))) uint2 plist[kWavesPerBlock][PT > 0 ? PT * kWave : 1];
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1076,6 +1164,10 @@ void checksum_kernel_split(const KernelArgs args) {
 
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
   uint32_t nrec = 0;
+  const uint32_t pl = lds_addr(&plist[wv][0]);
+  const bool list_ok = PT > 0 && args.tail_scatter && args.umem_size < kPatchMaxUmem;
+  int it = 0;              // tiles done by this wave
+  bool any_entry = false;  // wave-uniform: the patch list holds an entry
   // descriptors travel two tiles ahead
   uint4 d = *reinterpret_cast<const uint4 *>(args.descs + min(tile * kWave + lane, last));
   uint4 dn = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * kWave + lane, last));
@@ -1178,10 +1270,13 @@ void checksum_kernel_split(const KernelArgs args) {
     const bool huge = items > kItemsPerFrame;
     int32_t res = r.exists ? verdict : 0;
     LaneOut o = {res, false, slot, r.fp};
+    const bool to_list = list_ok && it < PT;   // wave-uniform
+    uint2 ent = make_uint2(0, 0);
     if (do_sum && !more) {
       const uint16_t c = check_of(h, PA, args.payload_mult);
       if (static_cast<uint32_t>(r.len) >= defer_min) {
-        res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
+        if (to_list) ent = patch_entry(args, r, h.u, c);
+        else res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
       } else {
         const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
         const uintptr_t ck = f0 + h.u + 6;
@@ -1272,7 +1367,8 @@ void checksum_kernel_split(const KernelArgs args) {
         const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
         const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
         if (static_cast<uint32_t>(r.len) >= defer_min) {
-          res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
+          if (to_list) ent = patch_entry(args, r, h.u, c);
+          else res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
         } else if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
                    sec + 64 <= c0 + 16 * W) {
           const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
@@ -1289,13 +1385,19 @@ void checksum_kernel_split(const KernelArgs args) {
       compiler_barrier();
     }
     nrec += store_result(args, f, f < args.n, res);
+    if (to_list) {
+      lds_store_u64(pl + 8 * (it * kWave + lane), ent);
+      any_entry |= __builtin_amdgcn_ballot_w64(ent.y != 0) != 0;
+    }
+    ++it;
     compiler_barrier();   // the next tile rewrites the slots
     d = dn;
     dn = dnn;
   }
   if (args.tail_scatter) {
+    if (any_entry) tail_patch_list(args, pl, min(it, PT), lane);
     if (__builtin_amdgcn_readfirstlane(nrec))
-      tail_scatter(args, blockIdx.x * kWavesPerBlock + wv, waves, lane);
+      tail_scatter(args, blockIdx.x * kWavesPerBlock + wv + (list_ok ? PT : 0) * waves, waves, lane);
   } else {
     publish_records(args, nrec, lane);
   }
