@@ -199,8 +199,9 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     # step i processes batch i % K
     umem, descs, lens = frames.device_batch(n * K, np.tile(lens_in, K), layout=layout, chunk=chunk or frames.CHUNK,
                                             seed=seed, device=dev)
-    hint = int(lens.max())
-    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint)
+    # the caller knows its batch: longest frame and mean length (xsknf_gpu_checksum_batch_lens)
+    hint, mean = int(lens.max()), int(lens_in.mean())
+    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint, frame_len_mean=mean)
     verdicts = torch.empty(n * K, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     umem_ptr, umem_size = umem.data_ptr(), umem.numel()
@@ -260,8 +261,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     import ctypes
     from xsknf_amd import _lib
     lib = _lib.load()
-    cfg = _lib.LaunchCfg()
-    _lib.check(lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(cfg)), "default_launch_cfg")
+    cfg = cs.launch_cfg()
     # one launch per step: every check in-line (mode 1), or deferred and patched
     # by each wave after its last tile (+16, split kernel)
     single_kernel = (cfg.fused_stores & 3) == 1 or bool(cfg.fused_stores & 16)
@@ -301,7 +301,11 @@ def time_workload(name, args, world, rank, dev, seed, primary):
 
     vh = verdicts[:n].cpu().numpy()
     counters = allreduce_sum_i64([n, bytes_len, int((vh == -1).sum()), int((vh >= 0).sum())], world)
+    shape = {"lanes_per_frame": cfg.lanes_per_frame, "chunks_per_lane": cfg.chunks_per_lane,
+             "items_in_flight": cfg.frames_per_group, "window_chunks": cfg.window_chunks & 15,
+             "frame_len_max": hint, "frame_len_mean": mean}
     return dict(name=name, desc=desc, n=n, K=K, lens=lens, bytes_len=bytes_len, step_ms=step_ms, stores=stores,
+                shape=shape,
                 step_ms_max=step_ms_max,
                 sum_ms=k_ms, single_kernel=single_kernel, family=family, wall_max=wall_max, counters=counters,
                 umem=umem, descs=descs, verdicts=verdicts, sample=sample, layout=layout, chunk=chunk, span=span)
@@ -516,7 +520,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_for(args.workload),
             "basis": "whole step (SURVEY.md 8(d)): sum(len + 22) per batch / HIP-event step time on the launch "
                      "stream; traffic = FETCH_SIZE/WRITE_SIZE of every kernel of one step",
-            "kernels": f"{prim['family']} ({prim['stores']})",
+            "kernels": f"{prim['family']} ({prim['stores']})", "launch_shape": prim["shape"],
             "alg_bytes_per_step": step_alg, "step_us": round(step_k_s * 1e6, 2),
             "summing_kernel_alone": kernel_alone, "attainable": attainable_for(prim)}
     cpu = None

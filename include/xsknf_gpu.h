@@ -149,6 +149,23 @@ struct xsknf_gpu_launch_cfg {
 /* The shape xsknf_gpu_checksum_batch() uses for a given frame_len_hint. */
 XSKNF_GPU_API int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg);
 
+/*
+ * xsknf_gpu_checksum_batch() for a caller that knows its batch's lengths: the
+ * longest frame and the mean length (0 = unknown, as xsknf_gpu_checksum_batch()).
+ * A batch of mostly long frames (mean >= 1280 B, up to 4 KiB) gets the split
+ * kernel's longer payload items, which suit a stream of long frames (1500 B:
+ * -1.7 %) but not a mix of mostly short ones such as IMIX (+15 %); a
+ * largest-frame hint alone cannot tell the two apart.  Results are identical
+ * either way: only the launch shape differs.
+ */
+XSKNF_GPU_API int xsknf_gpu_checksum_batch_lens(uint8_t *umem, uint64_t umem_size,
+		const struct xsknf_gpu_desc *descs, uint32_t n,
+		uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+		int32_t *verdicts, uint32_t frame_len_max, uint32_t frame_len_mean, void *stream);
+/* The shape xsknf_gpu_checksum_batch_lens() uses. */
+XSKNF_GPU_API int xsknf_gpu_launch_cfg_for_lens(uint32_t frame_len_max, uint32_t frame_len_mean,
+		struct xsknf_gpu_launch_cfg *cfg);
+
 /* xsknf_gpu_checksum_batch() with an explicit launch shape instead of a hint. */
 XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size,
 		const struct xsknf_gpu_desc *descs, uint32_t n,

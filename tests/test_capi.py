@@ -95,3 +95,26 @@ def test_ctx_argument_validation_without_gpu():
     assert lib.xsknf_gpu_ctx_create(ctypes.byref(ctx), 0, 0, 0, 0) == -errno.EINVAL
     assert lib.xsknf_gpu_ctx_process_batch(None, None, 0, 0, None, None) == -errno.EINVAL
     assert lib.xsknf_gpu_ctx_destroy(None) == -errno.EINVAL
+
+
+def test_launch_shape_for_lengths_without_gpu():
+    """xsknf_gpu_launch_cfg_for_lens: the mean length picks the split kernel's
+    item size for <= 4 KiB frames (16 x 3 for mostly long frames, 16 x 2 for a
+    mix or an unknown mean); the largest frame picks the kernel family."""
+    lib = _lib.load()
+
+    def shape(mx, mean):
+        c = _lib.LaunchCfg()
+        assert lib.xsknf_gpu_launch_cfg_for_lens(mx, mean, ctypes.byref(c)) == 0
+        return c.kernel, c.lanes_per_frame, c.chunks_per_lane, c.window_chunks, c.fused_stores
+
+    plain = _lib.LaunchCfg()
+    assert lib.xsknf_gpu_default_launch_cfg(1500, ctypes.byref(plain)) == 0
+    assert shape(1500, 0) == (plain.kernel, plain.lanes_per_frame, plain.chunks_per_lane,
+                              plain.window_chunks, plain.fused_stores)
+    assert shape(1500, 1500)[2] == 3 and shape(1500, 1500)[3] == 24
+    assert shape(1500, 352)[2] == 2 and shape(1500, 0)[2] == 2 and shape(1500, 1023)[2] == 2
+    assert shape(4000, 1024)[2] == 2 and shape(4000, 1280)[2] == 3
+    assert shape(9000, 9000)[3] == 20          # jumbo: 4-chunk window, whatever the mean
+    assert shape(64, 64)[1] == 1               # lane kernel
+    assert lib.xsknf_gpu_launch_cfg_for_lens(1500, 1500, None) == -errno.EINVAL

@@ -198,8 +198,9 @@ def test_full_size_configs_bit_exact(dev, name, n, length, layout):
     edge = frames.inject_edge_cases(b, 0.01, seed=n + len(name))
     umem.copy_(torch.from_numpy(host_in))
     descs.copy_(torch.from_numpy(host_descs.view(np.int64).reshape(n, 2)))
-    hint = int(lens.max())
-    v = Checksummer(frame_len_hint=hint).process_batch(umem, descs)
+    # the shape the bench runs: longest frame and mean length (xsknf_gpu_checksum_batch_lens)
+    hint, mean = int(lens.max()), int(lens.mean())
+    v = Checksummer(frame_len_hint=hint, frame_len_mean=mean).process_batch(umem, descs)
     torch.cuda.synchronize()
     _, ov = O.c_time_batch(host_in, host_descs, threads=16, reps=1)
     gv = v.cpu().numpy()
@@ -246,6 +247,8 @@ PRODUCT_SHAPES = [
     (16, 3, 1, 0, 0, 1, 24), (16, 3, 1, 0, 1, 1, 24), (16, 3, 1, 0, 2, 1, 24), (16, 3, 1, 0, 16, 1, 24),
     (16, 3, 1, 0, 18, 1, 24), (16, 3, 1, 0, 4, 1, 24),
     (16, 3, 2, 0, 0, 1, 20), (16, 3, 2, 0, 2, 1, 20), (16, 3, 2, 0, 20, 1, 20), (16, 3, 2, 0, 1, 1, 20),
+    # mostly long frames (mean >= 1 KiB): 16 x 3 items, two in flight, patch list of 8 tiles
+    (16, 3, 2, 0, 18, 1, 24), (16, 3, 2, 0, 2, 1, 24), (16, 3, 2, 0, 0, 1, 24), (16, 3, 2, 0, 1, 1, 24),
     # the lane kernel (short frames) under every store mode
     (1, 5, 2, 0, 1), (1, 5, 2, 0, 9), (1, 5, 2, 0, 5), (1, 5, 2, 0, 2), (1, 5, 2, 0, 0),
     # the zero-copy host path's small-batch group shapes
@@ -466,3 +469,32 @@ def test_concurrent_streams(dev):
     for k, ((umem, descs), (b, ou, ov, st)) in enumerate(zip(outs, jobs)):
         assert np.array_equal(res[3 * nstreams + k].cpu().numpy(), ov), f"stream {k}"
         assert np.array_equal(umem.cpu().numpy(), ou), f"stream {k}"
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 24), (16, 3, 2, 0, 18, 1, 24)], ids=_shape_id)
+def test_patch_list_overflow_takes_the_record_path(dev, shape):
+    """One block per CU: every wave gets more tiles than its LDS patch list
+    holds (6 or 8), so its later tiles park records in `verdicts` and are
+    patched by the record path (tail_scatter) after the list; every verdict and
+    byte still matches the oracle."""
+    import ctypes
+    from xsknf_amd import _lib
+    lib = _lib.load()
+    n = 600_000
+    umem, descs, lens = frames.device_batch(n, "imix", layout="aligned", device=dev, seed=31)
+    host = umem.cpu().numpy()
+    hd = descs.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1).copy()
+    frames.inject_edge_cases(frames.HostBatch(host, hd, "aligned"), 0.01, seed=32)
+    umem.copy_(torch.from_numpy(host))
+    descs.copy_(torch.from_numpy(hd.view(np.int64).reshape(n, 2)))
+    v = torch.empty(n, dtype=torch.int32, device=dev)
+    opts = _lib.CsumOpts(1, O.REDIRECT, 1, 0)
+    cfg = launch_cfg(shape, bpc=1)
+    assert lib.xsknf_gpu_checksum_batch_cfg(
+        ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), n, 0,
+        ctypes.byref(opts), ctypes.c_void_p(v.data_ptr()), ctypes.byref(cfg), None) == 0
+    torch.cuda.synchronize()
+    _, ov = O.c_time_batch(host, hd, threads=16, reps=1)
+    assert np.array_equal(v.cpu().numpy(), ov)
+    assert np.array_equal(umem.cpu().numpy(), host)

@@ -44,7 +44,7 @@ def main():
                     help="batches the timed launches cycle through (bench.py's rotation: keeps a small-frame "
                          "batch out of the Infinity Cache between launches)")
     a = ap.parse_args()
-    length, layout = WL[a.workload]
+    length, layout = WL[a.workload] if a.workload in WL else (int(a.workload), "aligned")
     dev = torch.device("cuda:0")
     K = max(1, a.rotate)
     base_lens = frames._lens(a.frames, length, __import__("numpy").random.default_rng(frames.SEED))

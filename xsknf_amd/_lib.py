@@ -21,6 +21,8 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_last_error",
     "xsknf_gpu_default_launch_cfg",
     "xsknf_gpu_checksum_batch_cfg",
+    "xsknf_gpu_checksum_batch_lens",
+    "xsknf_gpu_launch_cfg_for_lens",
     "xsknf_gpu_ctx_create",
     "xsknf_gpu_ctx_register_umem",
     "xsknf_gpu_ctx_process_batch",
@@ -111,6 +113,15 @@ def load() -> ctypes.CDLL:
     ]
     lib.xsknf_gpu_default_launch_cfg.restype = ctypes.c_int
     lib.xsknf_gpu_default_launch_cfg.argtypes = [ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]
+    lib.xsknf_gpu_checksum_batch_lens.restype = ctypes.c_int
+    lib.xsknf_gpu_checksum_batch_lens.argtypes = [
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+        ctypes.POINTER(CsumOpts), ctypes.c_void_p,
+        ctypes.c_uint32, ctypes.c_uint32,   # frame_len_max, frame_len_mean
+        ctypes.c_void_p,
+    ]
+    lib.xsknf_gpu_launch_cfg_for_lens.restype = ctypes.c_int
+    lib.xsknf_gpu_launch_cfg_for_lens.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(LaunchCfg)]
     lib.xsknf_gpu_checksum_batch_cfg.restype = ctypes.c_int
     lib.xsknf_gpu_checksum_batch_cfg.argtypes = [
         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,

@@ -110,10 +110,11 @@ class Checksummer:
     rewritten in place in `umem` and the verdict stored in `verdicts`."""
 
     def __init__(self, options: Optional[ChecksummerOptions] = None, num_interfaces: int = 1,
-                 frame_len_hint: int = 0):
+                 frame_len_hint: int = 0, frame_len_mean: int = 0):
         self.options = options or ChecksummerOptions()
         self.num_interfaces = int(num_interfaces)
         self.frame_len_hint = int(frame_len_hint)     # longest frame (0 = unknown)
+        self.frame_len_mean = int(frame_len_mean)     # mean length (0 = unknown): picks the launch shape
         self._lib = _lib.load()
 
     def csum_opts(self) -> _lib.CsumOpts:
@@ -126,11 +127,19 @@ class Checksummer:
         """Raw-pointer form (device pointers), asynchronous on `stream`."""
         hint = self.frame_len_hint if frame_len_hint is None else int(frame_len_hint)
         opts = self.csum_opts()
-        rc = self._lib.xsknf_gpu_checksum_batch(
+        rc = self._lib.xsknf_gpu_checksum_batch_lens(
             ctypes.c_void_p(umem_ptr), umem_size, ctypes.c_void_p(descs_ptr), n,
-            ingress_ifindex, ctypes.byref(opts), ctypes.c_void_p(verdicts_ptr), hint,
+            ingress_ifindex, ctypes.byref(opts), ctypes.c_void_p(verdicts_ptr), hint, self.frame_len_mean,
             ctypes.c_void_p(stream or None))
-        _lib.check(rc, "xsknf_gpu_checksum_batch")
+        _lib.check(rc, "xsknf_gpu_checksum_batch_lens")
+
+    def launch_cfg(self, frame_len_hint: Optional[int] = None) -> "_lib.LaunchCfg":
+        """The launch shape process_batch uses (xsknf_gpu_launch_cfg_for_lens)."""
+        hint = self.frame_len_hint if frame_len_hint is None else int(frame_len_hint)
+        cfg = _lib.LaunchCfg()
+        _lib.check(self._lib.xsknf_gpu_launch_cfg_for_lens(hint, self.frame_len_mean, ctypes.byref(cfg)),
+                   "xsknf_gpu_launch_cfg_for_lens")
+        return cfg
 
     def process_batch(self, umem, descs, ingress_ifindex: int = 0, verdicts=None,
                       frame_len_hint: Optional[int] = None, stream=None):

@@ -1060,17 +1060,24 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
 #endif
 constexpr int kPatchTiles = XSKNF_PATCH_TILES;   // 6 x 64 x 8 B x 4 waves = 12 KiB per block
 constexpr int kPatchT = XSKNF_PATCH_T;           // tiles whose sectors are in flight together
-constexpr uint32_t kPatchValid = 1u << 23, kPatchWhole = 1u << 22;
+constexpr uint32_t kPatchValid = 1u << 23, kPatchWhole = 1u << 22, kPatchInWin = 1u << 24;   // + window offset / 16 << 25
+#ifndef XSKNF_PATCH_LAST_SLOT
+#define XSKNF_PATCH_LAST_SLOT 0
+#endif
+constexpr bool kPatchLastSlot = XSKNF_PATCH_LAST_SLOT;   // the wave's last tile: sectors from its window slots
 constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with margin)
 
-__device__ __forceinline__ uint2 patch_entry(const KernelArgs &a, const FrameRef &r, int u, uint16_t c) {
+__device__ __forceinline__ uint2 patch_entry(const KernelArgs &a, const FrameRef &r, int u, uint16_t c, int wbytes) {
   const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
   const uintptr_t ck = f0 + static_cast<uintptr_t>(u) + 6;
   const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
   const uintptr_t base = reinterpret_cast<uintptr_t>(a.umem) & ~static_cast<uintptr_t>(63);
   const bool whole = sec >= f0 && sec + 64 <= f0 + static_cast<uintptr_t>(r.len) && (ck & 63) != 63;
+  const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
+  const bool in_win = whole && sec >= c0 && sec + 64 <= c0 + static_cast<uintptr_t>(wbytes);
   return make_uint2(static_cast<uint32_t>((sec - base) >> 6),
-                    kPatchValid | (whole ? kPatchWhole : 0u) | static_cast<uint32_t>((ck & 63) << 16) | c);
+                    kPatchValid | (whole ? kPatchWhole : 0u) | static_cast<uint32_t>((ck & 63) << 16) | c |
+                        (in_win ? kPatchInWin | static_cast<uint32_t>((sec - c0) >> 4) << 25 : 0u));
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -1089,7 +1096,11 @@ __device__ __forceinline__ uint2 lds_u64(uint32_t a) {
 // round, 4 lanes per frame, each frame's sector read and rewritten whole (one
 // non-temporal 64-byte store of 4 lanes), or its 2 check bytes where the sector
 // leaves the frame.  kPatchT tiles' sectors are in flight together.
-__device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t pl, int ntiles, int lane) {
+// last_slots: the LDS slots (stride `kslot`) still hold the windows of tile
+// ntiles - 1, the wave's last (kPatchLastSlot): its in-window sectors are taken
+// from there instead of being read again.
+__device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t pl, int ntiles, int lane,
+                                                bool last_in_slots, uint32_t area, uint32_t kslot) {
   const int piece = lane & 3;
   uint8_t *const base = args.umem - (reinterpret_cast<uintptr_t>(args.umem) & 63);   // keeps global addressing
   constexpr int T = kPatchT;
@@ -1106,7 +1117,10 @@ __device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t
         uint8_t *sec = base + (static_cast<uint64_t>(e.x) << 6);
         const bool whole = (e.y & (kPatchValid | kPatchWhole)) == (kPatchValid | kPatchWhole);
         mine[t][k] = whole ? sec + 16 * piece : sec + ((e.y >> 16) & 63);
-        if (whole) v[t][k] = load_nt(reinterpret_cast<const uint4 *>(mine[t][k]));
+        if (kPatchLastSlot && last_in_slots && t0 + t == ntiles - 1 && (e.y & kPatchInWin))
+          v[t][k] = lds_u128(area + kslot * (16 * k + (lane >> 2)) + 16 * ((e.y >> 25) & 7) + 16 * piece);
+        else if (whole)
+          v[t][k] = load_nt(reinterpret_cast<const uint4 *>(mine[t][k]));
       }
     }
 #pragma unroll
@@ -1148,7 +1162,9 @@ void checksum_kernel_split(const KernelArgs args) {
   __shared__ __attribute__((aligned(16))) uint16_t itemq[kWavesPerBlock][kItemCap];
   __shared__ __attribute__((aligned(16))) uint4 meta[kWavesPerBlock][kWave];
   __shared__ __attribute__((aligned(16))) uint32_t accb[kWavesPerBlock][kWave];
-  constexpr int PT = (W == 8 && U == 2 && !DMA && !PFW) ? kPatchTiles : 0;   // patch list tiles
+  // patch list tiles: 16 x 2 items fit 3 waves per SIMD (6 tiles per wave at 1M
+  // frames), 16 x 3 fit 2 (8 tiles per wave)
+  constexpr int PT = (W == 8 && U == 2 && !DMA && !PFW) ? (NCH == 2 ? kPatchTiles : 8) : 0;
   __shared__ __attribute__((aligned(16))) uint2 plist[kWavesPerBlock][PT > 0 ? PT * kWave : 1];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -1275,7 +1291,7 @@ void checksum_kernel_split(const KernelArgs args) {
     if (do_sum && !more) {
       const uint16_t c = check_of(h, PA, args.payload_mult);
       if (static_cast<uint32_t>(r.len) >= defer_min) {
-        if (to_list) ent = patch_entry(args, r, h.u, c);
+        if (to_list) ent = patch_entry(args, r, h.u, c, 16 * W);
         else res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
       } else {
         const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
@@ -1367,7 +1383,7 @@ void checksum_kernel_split(const KernelArgs args) {
         const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
         const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
         if (static_cast<uint32_t>(r.len) >= defer_min) {
-          if (to_list) ent = patch_entry(args, r, h.u, c);
+          if (to_list) ent = patch_entry(args, r, h.u, c, 16 * W);
           else res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
         } else if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
                    sec + 64 <= c0 + 16 * W) {
@@ -1395,7 +1411,7 @@ void checksum_kernel_split(const KernelArgs args) {
     dn = dnn;
   }
   if (args.tail_scatter) {
-    if (any_entry) tail_patch_list(args, pl, min(it, PT), lane);
+    if (any_entry) tail_patch_list(args, pl, min(it, PT), lane, it <= PT, area, kSlot);
     if (__builtin_amdgcn_readfirstlane(nrec))
       tail_scatter(args, blockIdx.x * kWavesPerBlock + wv + (list_ok ? PT : 0) * waves, waves, lane);
   } else {
@@ -1802,7 +1818,8 @@ struct Variant {
 #define XSKNF_SP(L, N, U) {L, N, U, 2, &launch_split<8, L, N, U, true, false, true>, XSKNF_GPU_KERNEL_SPLIT, 24}
 const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
-    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
+    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 16, 3, 1, 1),
+    XSKNF_S(4, 16, 3, 2, 1),
     // ... the lane kernel for short frames ...
     XSKNF_L(5, 2),
     // ... and the zero-copy host path's small-batch group shapes (host_path.hip)
@@ -1814,7 +1831,7 @@ const Variant kVariants[] = {
     XSKNF_S(7, 16, 2, 1, 0), XSKNF_S(4, 16, 3, 1, 0), XSKNF_S(4, 8, 2, 2, 0),
     XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
-    XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
+    XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
     XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
     XSKNF_SP(16, 2, 2), XSKNF_SP(16, 3, 1),         // window prefetch: +3-6 us on 1500 / IMIX / 570 (tune_pfw)
     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
@@ -1849,8 +1866,17 @@ const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   return nullptr;
 }
 
-// Default shape for a batch whose longest frame is `hint` bytes.
-void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
+// Mean frame length from which a batch of <= 4 KiB frames takes 16 x 3 items
+// (two in flight, 188 VGPRs: 2 waves per SIMD, 8 tiles per wave at 1M frames)
+// instead of 16 x 2 (3 waves per SIMD).  Same process, interleaved: 1500 B
+// 283.0 vs 287.7 us, 288.2-296.9 vs 290.7-302.6; 1024 B 211.8-214.7 vs
+// 206.5-207.4; 800 B a tie; 570 B 159.9 vs 144.4; IMIX 127.6 vs 110.7
+// (profiles/r02/ab_nch3.jsonl, ab_nch3_lengths.jsonl).
+constexpr uint32_t kLongMean = 1280;
+
+// Default shape for a batch whose longest frame is `hint` bytes and whose
+// mean length is `mean` (0 = unknown: the shape that suits any mix).
+void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   c.frames_per_group = 4;
   c.blocks_per_cu = 8;
   c.lds_ring = 0;
@@ -1875,7 +1901,8 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c) {
     c.kernel = XSKNF_GPU_KERNEL_AUTO;
     c.lanes_per_frame = 1; c.window_chunks = 0; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
   } else if (hint + 15 <= 4096) {
-    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
+    c.window_chunks = 8 + 16; c.chunks_per_lane = mean >= kLongMean ? 3 : 2; c.frames_per_group = 2;
+    c.fused_stores = 2 + 16;
   } else {
     c.window_chunks = 4 + 16; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
   }
@@ -1983,6 +2010,25 @@ int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct
 int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg) {
   if (!cfg) return -EINVAL;
   xsknf_gpu::default_cfg(frame_len_hint ? frame_len_hint : 2048u, *cfg);
+  return 0;
+}
+
+int xsknf_gpu_checksum_batch_lens(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
+                                  uint32_t n, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+                                  int32_t *verdicts, uint32_t frame_len_max, uint32_t frame_len_mean,
+                                  void *stream) {
+  xsknf_gpu::KernelArgs a;
+  const int rc = xsknf_gpu::prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
+  if (rc != 0) return rc < 0 ? rc : 0;
+  xsknf_gpu_launch_cfg cfg;
+  xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, cfg, frame_len_mean);
+  return xsknf_gpu::run(a, cfg, stream);
+}
+
+int xsknf_gpu_launch_cfg_for_lens(uint32_t frame_len_max, uint32_t frame_len_mean,
+                                  struct xsknf_gpu_launch_cfg *cfg) {
+  if (!cfg) return -EINVAL;
+  xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, *cfg, frame_len_mean);
   return 0;
 }
 

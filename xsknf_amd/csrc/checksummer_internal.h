@@ -45,7 +45,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
             uint32_t ingress_ifindex, const xsknf_csum_opts *opts, int32_t *verdicts);
 // Launch the shape `cfg` (summing kernel + scatter pass unless a.no_scatter).
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream);
-void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c);
+void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean = 0);
 void set_error(hipError_t e, const char *where);
 void set_error_text(const char *text);
 
