@@ -57,7 +57,7 @@ def main():
     n = a.frames
     hint = int(lens.max())
     dflt = _lib.LaunchCfg()
-    lib.xsknf_gpu_default_launch_cfg(hint, ctypes.byref(dflt))
+    lib.xsknf_gpu_launch_cfg_for_lens(hint, int(lens.mean()), ctypes.byref(dflt))   # the product's choice
     shapes = [(dflt.lanes_per_frame, dflt.chunks_per_lane, dflt.frames_per_group, dflt.lds_ring,
                dflt.fused_stores, dflt.kernel, dflt.window_chunks)]
     for t in [x for x in a.variants.split(":") if x]:

@@ -1059,7 +1059,7 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
 #define XSKNF_PATCH_T 2
 #endif
 constexpr int kPatchTiles = XSKNF_PATCH_TILES;   // 6 x 64 x 8 B x 4 waves = 12 KiB per block
-constexpr int kPatchT = XSKNF_PATCH_T;           // tiles whose sectors are in flight together
+constexpr int kPatchT = XSKNF_PATCH_T;           // tiles whose sectors are in flight together (3, 4: no gain, r02 ab_tail2)
 constexpr uint32_t kPatchValid = 1u << 23, kPatchWhole = 1u << 22, kPatchInWin = 1u << 24;   // + window offset / 16 << 25
 #ifndef XSKNF_PATCH_LAST_SLOT
 #define XSKNF_PATCH_LAST_SLOT 0
@@ -1132,7 +1132,7 @@ __device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t
           const int o = static_cast<int>((info[t][k] >> 16) & 63) - 16 * piece;
           uint4 w = put_byte(v[t][k], o, c);
           w = put_byte(w, o + 1, c >> 8);
-          store_nt16(mine[t][k], w);
+          store_nt16(mine[t][k], w);   // plain (write-back) stores: 1500 B +20 us, IMIX +8 (r02 ab_tail2)
         } else if ((info[t][k] & kPatchValid) && piece == 0) {
           mine[t][k][0] = static_cast<uint8_t>(c);
           mine[t][k][1] = static_cast<uint8_t>(c >> 8);
