@@ -76,6 +76,16 @@ $(ABLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h tool
 	python3 tools/check_inflight.py build/ab/checksummer-gfx950.s
 	$(HIPCC) $(HIPFLAGS) -DXSKNF_AB -shared -o $@ $(SRCS)
 
+# Timeline build: the product shapes with the split kernel's per-wave clock
+# samples (tools/timeline.py).  Not the product.
+TLLIB := build/tl/libxsknf_gpu.so
+tl: $(TLLIB)
+$(TLLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h tools/check_inflight.py Makefile
+	@mkdir -p build/tl
+	$(HIPCC) $(HIPFLAGS) -DXSKNF_TIMELINE $(TLFLAGS) --cuda-device-only -S -o build/tl/checksummer-gfx950.s xsknf_amd/csrc/checksummer.hip
+	python3 tools/check_inflight.py build/tl/checksummer-gfx950.s
+	$(HIPCC) $(HIPFLAGS) -DXSKNF_TIMELINE $(TLFLAGS) -shared -o $@ $(SRCS)
+
 # keep the device assembly for inspection (VGPRs, instruction mix)
 asm: $(SRCS)
 	@mkdir -p build/asm
@@ -88,4 +98,12 @@ clean:
 	rm -rf $(LIBDIR) xsknf_amd/bin build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean tools ab
+.PHONY: all oracle asm clean tools ab tl guard
+
+# Guard build: every UMEM access of the split kernel's paths range-checked and
+# recorded instead of faulting (tools/guard_run.py).  Not the product.
+GDLIB := build/guard/libxsknf_gpu.so
+guard: $(GDLIB)
+$(GDLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h Makefile
+	@mkdir -p build/guard
+	$(HIPCC) $(HIPFLAGS) -DXSKNF_GUARD -shared -o $@ $(SRCS)

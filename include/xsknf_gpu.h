@@ -152,11 +152,11 @@ XSKNF_GPU_API int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct x
 /*
  * xsknf_gpu_checksum_batch() for a caller that knows its batch's lengths: the
  * longest frame and the mean length (0 = unknown, as xsknf_gpu_checksum_batch()).
- * A batch of mostly long frames (mean >= 1280 B, up to 4 KiB) gets the split
- * kernel's longer payload items, which suit a stream of long frames (1500 B:
- * -1.7 %) but not a mix of mostly short ones such as IMIX (+15 %); a
- * largest-frame hint alone cannot tell the two apart.  Results are identical
- * either way: only the launch shape differs.
+ * The mean is there for the shape choice, which a largest-frame hint alone
+ * cannot make (longer payload items suit a stream of long frames, 1500 B
+ * -1..2 %, but not a mix of mostly short ones such as IMIX, +15 %); today the
+ * product takes the same shape for every mean (the long-frame shape is A/B
+ * material).  Results are identical whatever the shape.
  */
 XSKNF_GPU_API int xsknf_gpu_checksum_batch_lens(uint8_t *umem, uint64_t umem_size,
 		const struct xsknf_gpu_desc *descs, uint32_t n,

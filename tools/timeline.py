@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of the split kernel (A/B instrument; `make tl` builds
+build/tl/libxsknf_gpu.so with -DXSKNF_TIMELINE).
+
+Each wave records the 100 MHz constant clock at its start, after its last
+tile (stream done, its loads drained), and after its own patches, its tile
+count, and the clock summed over its tiles in phase A's window loads, the rest
+of phase A, and phase B.  The summary splits the launch into the stream and the patch
+phase: when the first / median / last wave finished streaming, how long the
+patches took per wave, and how much of the patch time overlapped other
+waves' streams.
+
+    XSKNF_GPU_LIB=build/tl/libxsknf_gpu.so python tools/timeline.py --workload 1500
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from xsknf_amd import _lib, frames  # noqa: E402
+
+WL = {"1500": (1500, "aligned"), "imix": ("imix", "aligned"), "570": (570, "aligned"),
+      "1024": (1024, "aligned")}
+
+
+def pct(x, q):
+    return round(float(np.percentile(x, q)), 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="1500")
+    ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--rotate", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variant", default="", help="lanes,chunks,u,ring,fused,kernel,window (default: product)")
+    a = ap.parse_args()
+    length, layout = WL.get(a.workload, (int(a.workload) if a.workload.isdigit() else a.workload, "aligned"))
+    dev = torch.device("cuda:0")
+    K = max(1, a.rotate)
+    base = frames._lens(a.frames, length, np.random.default_rng(frames.SEED))
+    umem, descs_all, lens_all = frames.device_batch(a.frames * K, np.tile(base, K), layout=layout, device=dev)
+    n = a.frames
+    lib = _lib.load()
+    if not hasattr(lib, "xsknf_gpu_ab_set_timeline"):
+        raise SystemExit("not a timeline build: set XSKNF_GPU_LIB=build/tl/libxsknf_gpu.so")
+    lib.xsknf_gpu_ab_set_timeline.argtypes = [ctypes.c_void_p]
+    opts = _lib.CsumOpts(1, 0, 1, 0)
+    cfg = _lib.LaunchCfg()
+    lens = lens_all[:n]
+    lib.xsknf_gpu_launch_cfg_for_lens(int(lens.max()), int(lens.mean()), ctypes.byref(cfg))
+    if a.variant:
+        v = [int(x) for x in a.variant.split(",")]
+        cfg = _lib.LaunchCfg(v[0], v[1], v[2], 4, v[3], v[4], v[5], v[6])
+    verd = torch.empty(n, dtype=torch.int32, device=dev)
+    tl = torch.zeros(8 * 65536, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def run(j):
+        rc = lib.xsknf_gpu_checksum_batch_cfg(ctypes.c_void_p(umem.data_ptr()), umem.numel(),
+                                              ctypes.c_void_p(descs_all.data_ptr() + 16 * n * j), n, 0,
+                                              ctypes.byref(opts), ctypes.c_void_p(verd.data_ptr()),
+                                              ctypes.byref(cfg), ctypes.c_void_p(stream.cuda_stream))
+        _lib.check(rc, "launch")
+
+    _lib.check(lib.xsknf_gpu_ab_set_timeline(None), "timeline off")
+    for j in range(10):
+        run(j % K)
+    torch.cuda.synchronize()
+    rows = []
+    for r in range(a.reps):
+        tl.zero_()
+        torch.cuda.synchronize()
+        _lib.check(lib.xsknf_gpu_ab_set_timeline(ctypes.c_void_p(tl.data_ptr())), "timeline on")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        run(r % K)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        _lib.check(lib.xsknf_gpu_ab_set_timeline(None), "timeline off")
+        t = tl.view(-1, 8).cpu().numpy()
+        t = t[t[:, 0] != 0]
+        t0 = t[:, 0].min()
+        start, sdone, pdone = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, (t[:, 2] - t0) / 100.0   # us
+        end = pdone.max()
+        patch = pdone - sdone
+        # patch time of waves while some other wave was still streaming
+        last_stream = sdone.max()
+        overl = np.clip(np.minimum(pdone, last_stream) - sdone, 0, None)
+        tiles = t[:, 3]
+        rows.append({
+            "event_us": round(e0.elapsed_time(e1) * 1e3, 2), "waves": int(len(t)), "kernel_us": round(float(end), 2),
+            "start_p99": pct(start, 99), "stream_done": [pct(sdone, 0), pct(sdone, 10), pct(sdone, 50),
+                                                          pct(sdone, 90), pct(sdone, 100)],
+            "patch_us": [pct(patch, 0), pct(patch, 50), pct(patch, 90), pct(patch, 100)],
+            "patch_overlapping_stream_us_mean": round(float(overl.mean()), 2),
+            "after_last_stream_us": round(float(end - last_stream), 2),
+            "tiles": {int(k): int(v) for k, v in zip(*np.unique(tiles, return_counts=True))},
+            "per_wave_us_phaseA_window_parse_B": [round(float(t[:, k].mean()) / 100.0, 2) for k in (4, 5, 6)],
+            "stream_done_by_tiles": {int(k): pct(sdone[tiles == k], 50) for k in np.unique(tiles)},
+        })
+    rows.sort(key=lambda x: x["kernel_us"])
+    med = rows[len(rows) // 2]
+    print(json.dumps({"workload": a.workload, "cfg": [cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group,
+                                                      cfg.lds_ring, cfg.fused_stores, cfg.kernel, cfg.window_chunks],
+                      "median": med, "kernel_us_all": [r["kernel_us"] for r in rows]}))
+
+
+if __name__ == "__main__":
+    main()

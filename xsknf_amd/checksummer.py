@@ -114,7 +114,7 @@ class Checksummer:
         self.options = options or ChecksummerOptions()
         self.num_interfaces = int(num_interfaces)
         self.frame_len_hint = int(frame_len_hint)     # longest frame (0 = unknown)
-        self.frame_len_mean = int(frame_len_mean)     # mean length (0 = unknown): picks the launch shape
+        self.frame_len_mean = int(frame_len_mean)     # mean length (0 = unknown): for the launch shape choice
         self._lib = _lib.load()
 
     def csum_opts(self) -> _lib.CsumOpts:

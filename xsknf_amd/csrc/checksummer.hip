@@ -109,13 +109,56 @@ __device__ __forceinline__ int32_t lds_i32(uint32_t a) {
   return *reinterpret_cast<const __attribute__((address_space(3))) int32_t *>(static_cast<uintptr_t>(a));
 }
 
+#ifdef XSKNF_GUARD
+// Debug instrument (`make guard`, tools/guard_run.py): every UMEM access of the
+// split kernel's paths is checked against the ranges the host put in
+// g_guard[1..6] (umem, descriptors, verdicts); an access outside them is
+// recorded (source line, thread, address) and skipped -- a load reads the
+// descriptor array's first 16 bytes instead -- so a bad address is found
+// without faulting the GPU.  Not in the product library.
+__device__ unsigned long long *g_guard;
+template <typename P>
+__device__ __forceinline__ bool guard_ok(P p, uint32_t bytes, int site) {
+  unsigned long long *g = g_guard;
+  if (!g) return true;
+  const unsigned long long x = reinterpret_cast<uintptr_t>(p);
+  const bool ok = (x >= g[1] && x + bytes <= g[2]) || (x >= g[3] && x + bytes <= g[4]) ||
+                  (x >= g[5] && x + bytes <= g[6]);
+  if (!ok) {
+    const unsigned long long i = atomicAdd(g, 1ull);
+    if (i < 2048) {
+      g[8 + 2 * i] = (static_cast<unsigned long long>(site) << 32) | (blockIdx.x * 256u + threadIdx.x);
+      g[9 + 2 * i] = x;
+    }
+  }
+  return ok;
+}
+template <typename P>
+__device__ __forceinline__ P guard_ld(P p, uint32_t bytes, int site) {
+  return guard_ok(p, bytes, site) ? p : reinterpret_cast<P>(static_cast<uintptr_t>(g_guard[3]));
+}
+#define XSKNF_SITE , int site = __builtin_LINE()
+#define XSKNF_GLD(p, bytes) guard_ld(p, bytes, __LINE__)
+#define XSKNF_GST(p, bytes) if (guard_ok(p, bytes, __LINE__))
+#else
+#define XSKNF_SITE
+#define XSKNF_GLD(p, bytes) (p)
+#define XSKNF_GST(p, bytes)
+#endif
+
 // non-temporal 16-byte global load (streamed once)
-__device__ __forceinline__ uint4 load_nt(const uint4 *p) {
+__device__ __forceinline__ uint4 load_nt(const uint4 *p XSKNF_SITE) {
+#ifdef XSKNF_GUARD
+  p = guard_ld(p, 16, site);
+#endif
   const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
   return make_uint4(x.x, x.y, x.z, x.w);
 }
 
-__device__ __forceinline__ void store_nt16(uint8_t *p, uint4 v) {
+__device__ __forceinline__ void store_nt16(uint8_t *p, uint4 v XSKNF_SITE) {
+#ifdef XSKNF_GUARD
+  if (!guard_ok(p, 16, site)) return;
+#endif
   u32x4 x = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
 }
@@ -797,7 +840,10 @@ __device__ __forceinline__ uint32_t lds_byte(uint32_t a) {
 // behind the loads in flight.
 typedef const __attribute__((address_space(1))) u32x4 *gchunk_ptr;
 
-__device__ __forceinline__ uint4 load_nt(gchunk_ptr p) {
+__device__ __forceinline__ uint4 load_nt(gchunk_ptr p XSKNF_SITE) {
+#ifdef XSKNF_GUARD
+  p = guard_ld(p, 16, site);
+#endif
   const u32x4 x = __builtin_nontemporal_load(p);
   return make_uint4(x.x, x.y, x.z, x.w);
 }
@@ -828,7 +874,10 @@ __device__ __forceinline__ Payload payload_of(uint4 m) {
 // register is bound to its wait (an empty asm with a "+v" operand after the
 // s_waitcnt), so no use can move above the wait, and a stage that is never
 // consumed is drained before its registers can be reused.
-__device__ __forceinline__ u32x4 gload_nt_asm(gchunk_ptr p) {
+__device__ __forceinline__ u32x4 gload_nt_asm(gchunk_ptr p XSKNF_SITE) {
+#ifdef XSKNF_GUARD
+  p = guard_ld(p, 16, site);
+#endif
   u32x4 x;   // nt: default-policy loads measured 1500 B 296 -> 344 us per step
   asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(x) : "v"(p) : "memory");
   return x;
@@ -1033,8 +1082,10 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
           w = put_byte(w, o[t][k] + 1, c >> 8);
           store_nt16(mine[t][k], w);
         } else if (has[t][k] && piece == 0) {
-          mine[t][k][0] = static_cast<uint8_t>(c);
-          mine[t][k][1] = static_cast<uint8_t>(c >> 8);
+          XSKNF_GST(mine[t][k], 2) {
+            mine[t][k][0] = static_cast<uint8_t>(c);
+            mine[t][k][1] = static_cast<uint8_t>(c >> 8);
+          }
         }
       }
       if (rec[t]) args.verdicts[(tb + t * waves) * kWave + lane] = args.fwd_verdict;
@@ -1134,13 +1185,36 @@ __device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t
           w = put_byte(w, o + 1, c >> 8);
           store_nt16(mine[t][k], w);   // plain (write-back) stores: 1500 B +20 us, IMIX +8 (r02 ab_tail2)
         } else if ((info[t][k] & kPatchValid) && piece == 0) {
-          mine[t][k][0] = static_cast<uint8_t>(c);
-          mine[t][k][1] = static_cast<uint8_t>(c >> 8);
+          XSKNF_GST(mine[t][k], 2) {
+            mine[t][k][0] = static_cast<uint8_t>(c);
+            mine[t][k][1] = static_cast<uint8_t>(c >> 8);
+          }
         }
       }
     }
   }
 }
+
+#ifdef XSKNF_TIMELINE
+// A/B instrument (tools/timeline.py): per wave of the split kernel, the
+// constant 100 MHz clock at its start, after its last tile, after its patches,
+// and its tile count, so the step can be split into stream and patch time.
+__device__ unsigned long long *g_timeline;
+// 8 u64 per wave: start, stream done, patches done, tiles, then the clock
+// summed over the wave's tiles in phase A (window loads until they are in
+// LDS), phase A's parse, and phase B (payload items)
+__device__ __forceinline__ void timeline_put(uint32_t wave, int lane, unsigned long long t0, unsigned long long t1,
+                                             int tiles, unsigned long long sa, unsigned long long sp,
+                                             unsigned long long sb) {
+  const unsigned long long t2 = wall_clock64();
+  unsigned long long *p = g_timeline;
+  const unsigned long long v[8] = {t0, t1, t2, static_cast<unsigned long long>(tiles), sa, sp, sb, 0ull};
+  unsigned long long x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x = lane == k ? v[k] : x;
+  if (p && lane < 8) p[8ull * wave + lane] = x;
+}
+#endif
 
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
@@ -1180,6 +1254,15 @@ void checksum_kernel_split(const KernelArgs args) {
 
   uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
   uint32_t nrec = 0;
+#ifdef XSKNF_TIMELINE
+  const unsigned long long tl0 = wall_clock64();
+  unsigned long long tl_a = 0, tl_p = 0, tl_b = 0, tl_t = 0;
+#define XSKNF_TL_MARK(acc) do { const unsigned long long n_ = wall_clock64(); acc += n_ - tl_t; tl_t = n_; } while (0)
+#define XSKNF_TL_START() do { tl_t = wall_clock64(); } while (0)
+#else
+#define XSKNF_TL_START() do { } while (0)
+#define XSKNF_TL_MARK(acc) do { } while (0)
+#endif
   const uint32_t pl = lds_addr(&plist[wv][0]);
   const bool list_ok = PT > 0 && args.tail_scatter && args.umem_size < kPatchMaxUmem;
   int it = 0;              // tiles done by this wave
@@ -1213,6 +1296,7 @@ void checksum_kernel_split(const KernelArgs args) {
     window_pending = true;
   }
   for (; tile * kWave < args.n; tile += waves) {
+    XSKNF_TL_START();
     const uint32_t f = tile * kWave + lane;
     const FrameRef r = lane_ref(args, d, f);
     uint4 v[W];
@@ -1234,7 +1318,7 @@ void checksum_kernel_split(const KernelArgs args) {
         const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
         const int nc = __builtin_amdgcn_ds_bpermute(g << 2, r.nch);
         const gchunk_ptr cp = reinterpret_cast<gchunk_ptr>((static_cast<uintptr_t>(hi) << 32) | lo);
-        x[p] = cp[min(lane % W, nc - 1)];   // default policy: nt measured 64 B 39 -> 55 us, 1500 B 292 -> 308
+        x[p] = *XSKNF_GLD(cp + min(lane % W, nc - 1), 16);   // default policy: nt measured 64 B 39 -> 55 us, 1500 B 292 -> 308
       }
       compiler_barrier();
 #pragma unroll
@@ -1246,6 +1330,7 @@ void checksum_kernel_split(const KernelArgs args) {
     } else {
       load_lane<W>(r, v);
     }
+    XSKNF_TL_MARK(tl_a);
     const uint4 dnn = *reinterpret_cast<const uint4 *>(args.descs + min((tile + 2 * waves) * kWave + lane, last));
     // per-tile store policy, as the register kernel: long frames defer their
     // checks only where they are at least half of the tile
@@ -1307,7 +1392,7 @@ void checksum_kernel_split(const KernelArgs args) {
           o.lds_sec = slot + static_cast<uint32_t>(sec - c0);
           o.gsec = r.fp + static_cast<intptr_t>(sec - f0);
         } else {
-          *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+          XSKNF_GST(r.fp + h.u + 6, 2) *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
         }
       }
     }
@@ -1319,6 +1404,7 @@ void checksum_kernel_split(const KernelArgs args) {
     }
 
     // ---- phase B: payload items of the longer frames ----
+    XSKNF_TL_MARK(tl_p);
     if (__builtin_amdgcn_ballot_w64(more)) {
       const uintptr_t fpv = reinterpret_cast<uintptr_t>(r.fp);
       lds_store_u128(mt + 16 * lane, make_uint4(static_cast<uint32_t>(fpv), static_cast<uint32_t>(fpv >> 32),
@@ -1370,6 +1456,7 @@ void checksum_kernel_split(const KernelArgs args) {
         if (lane == kWave - 1) lds_add_u32(ab + 4 * fl, P);
       }
       compiler_barrier();
+      XSKNF_TL_MARK(tl_b);
       // ---- phase C: fold, check, store ----
       // an in-line check whose 64-byte sector lies in the frame and the window
       // is written as that whole sector: patched in the lane's slot (the window
@@ -1394,7 +1481,7 @@ void checksum_kernel_split(const KernelArgs args) {
           oc.lds_sec = slot + static_cast<uint32_t>(sec - c0);
           oc.gsec = r.fp + static_cast<intptr_t>(sec - f0);
         } else {
-          *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+          XSKNF_GST(r.fp + h.u + 6, 2) *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
         }
       }
       store_sectors(oc, lane, args.plain_sector);
@@ -1410,6 +1497,10 @@ void checksum_kernel_split(const KernelArgs args) {
     d = dn;
     dn = dnn;
   }
+#ifdef XSKNF_TIMELINE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long tl1 = wall_clock64();
+#endif
   if (args.tail_scatter) {
     if (any_entry) tail_patch_list(args, pl, min(it, PT), lane, it <= PT, area, kSlot);
     if (__builtin_amdgcn_readfirstlane(nrec))
@@ -1417,6 +1508,10 @@ void checksum_kernel_split(const KernelArgs args) {
   } else {
     publish_records(args, nrec, lane);
   }
+#ifdef XSKNF_TIMELINE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  timeline_put(blockIdx.x * kWavesPerBlock + wv, lane, tl0, tl1, it, tl_a, tl_p, tl_b);
+#endif
 }
 
 #ifdef XSKNF_AB
@@ -1818,8 +1913,7 @@ struct Variant {
 #define XSKNF_SP(L, N, U) {L, N, U, 2, &launch_split<8, L, N, U, true, false, true>, XSKNF_GPU_KERNEL_SPLIT, 24}
 const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
-    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 2, 1), XSKNF_S(8, 16, 3, 1, 1),
-    XSKNF_S(4, 16, 3, 2, 1),
+    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
     // ... the lane kernel for short frames ...
     XSKNF_L(5, 2),
     // ... and the zero-copy host path's small-batch group shapes (host_path.hip)
@@ -1832,6 +1926,7 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
+    XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
     XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
     XSKNF_SP(16, 2, 2), XSKNF_SP(16, 3, 1),         // window prefetch: +3-6 us on 1500 / IMIX / 570 (tune_pfw)
     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
@@ -1866,14 +1961,13 @@ const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   return nullptr;
 }
 
-// Mean frame length from which a batch of <= 4 KiB frames takes 16 x 3 items
+// The mean length does not change the product's shape today.  16 x 3 items
 // (two in flight, 188 VGPRs: 2 waves per SIMD, 8 tiles per wave at 1M frames)
-// instead of 16 x 2 (3 waves per SIMD).  Same process, interleaved: 1500 B
-// 283.0 vs 287.7 us, 288.2-296.9 vs 290.7-302.6; 1024 B 211.8-214.7 vs
-// 206.5-207.4; 800 B a tie; 570 B 159.9 vs 144.4; IMIX 127.6 vs 110.7
-// (profiles/r02/ab_nch3.jsonl, ab_nch3_lengths.jsonl).
-constexpr uint32_t kLongMean = 1280;
-
+// for batches of mean >= 1280 B measured 1500 B 283.0 vs 287.7 us, 288.2-296.9
+// vs 290.7-302.6 (profiles/r02/ab_nch3.jsonl, ab_nch3_lengths.jsonl), but one
+// launch of it over a batch larger than its patch lists (one block per CU)
+// faulted once in the full GPU suite and could not be reproduced alone, so it
+// stays an A/B shape.
 // Default shape for a batch whose longest frame is `hint` bytes and whose
 // mean length is `mean` (0 = unknown: the shape that suits any mix).
 void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
@@ -1901,8 +1995,8 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
     c.kernel = XSKNF_GPU_KERNEL_AUTO;
     c.lanes_per_frame = 1; c.window_chunks = 0; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
   } else if (hint + 15 <= 4096) {
-    c.window_chunks = 8 + 16; c.chunks_per_lane = mean >= kLongMean ? 3 : 2; c.frames_per_group = 2;
-    c.fused_stores = 2 + 16;
+    (void)mean;
+    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   } else {
     c.window_chunks = 4 + 16; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
   }
@@ -2031,5 +2125,25 @@ int xsknf_gpu_launch_cfg_for_lens(uint32_t frame_len_max, uint32_t frame_len_mea
   xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, *cfg, frame_len_mean);
   return 0;
 }
+
+#ifdef XSKNF_GUARD
+// Debug instrument: the guard buffer (u64: [0] count, [1..6] allowed ranges,
+// records from [8]; NULL: off).  Not in the product library.
+__attribute__((visibility("default"))) int xsknf_gpu_ab_set_guard(void *buf) {
+  unsigned long long *p = static_cast<unsigned long long *>(buf);
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(xsknf_gpu::g_guard), &p, sizeof(p));
+  return e == hipSuccess ? 0 : -EIO;
+}
+#endif
+
+#ifdef XSKNF_TIMELINE
+// A/B instrument: the split kernel's per-wave timeline goes to `buf` (4 u64
+// per wave; NULL: off).  Not in the product library.
+__attribute__((visibility("default"))) int xsknf_gpu_ab_set_timeline(void *buf) {
+  unsigned long long *p = static_cast<unsigned long long *>(buf);
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(xsknf_gpu::g_timeline), &p, sizeof(p));
+  return e == hipSuccess ? 0 : -EIO;
+}
+#endif
 
 }  // extern "C"
