@@ -126,7 +126,9 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * x `chunks_per_lane` chunks dealt to the wave's lane groups, `frames_per_group`
  * items per group in flight (any mix of lengths keeps every lane busy);
  * `window_chunks` + 16 loads the windows transposed (W lanes per frame, one
- * coalesced request).  Only instantiated shapes are accepted (-EINVAL
+ * coalesced request); + 32 (with + 16, W = 8, 16 x 2 items, two in flight)
+ * launches one 12-wave block per CU whose waves draw the CU's tiles from a
+ * shared pool (the default up to 4 KiB frames).  Only instantiated shapes are accepted (-EINVAL
  * otherwise); every shape gives identical results.
  */
 #define XSKNF_GPU_RECORD_TAG 0x40000000u       /* bits 31..30 = 01 */

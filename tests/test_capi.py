@@ -113,7 +113,7 @@ def test_launch_shape_for_lengths_without_gpu():
     for mean in (0, 352, 1023, 1280, 1500):
         assert shape(1500, mean) == (plain.kernel, plain.lanes_per_frame, plain.chunks_per_lane,
                                      plain.window_chunks, plain.fused_stores)
-    assert shape(1500, 1500)[2] == 2 and shape(1500, 1500)[3] == 24
+    assert shape(1500, 1500)[2] == 2 and shape(1500, 1500)[3] == 56
     assert shape(4000, 1024)[2] == 2 and shape(4000, 1280)[2] == 2
     assert shape(9000, 9000)[3] == 20          # jumbo: 4-chunk window, whatever the mean
     assert shape(64, 64)[1] == 1               # lane kernel

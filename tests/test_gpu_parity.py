@@ -247,6 +247,8 @@ PRODUCT_SHAPES = [
     (16, 3, 1, 0, 0, 1, 24), (16, 3, 1, 0, 1, 1, 24), (16, 3, 1, 0, 2, 1, 24), (16, 3, 1, 0, 16, 1, 24),
     (16, 3, 1, 0, 18, 1, 24), (16, 3, 1, 0, 4, 1, 24),
     (16, 3, 2, 0, 0, 1, 20), (16, 3, 2, 0, 2, 1, 20), (16, 3, 2, 0, 20, 1, 20), (16, 3, 2, 0, 1, 1, 20),
+    # one 12-wave block per CU sharing the CU's tiles (window + 32)
+    (16, 2, 2, 0, 18, 1, 56), (16, 2, 2, 0, 2, 1, 56), (16, 2, 2, 0, 0, 1, 56), (16, 2, 2, 0, 1, 1, 56),
     # the lane kernel (short frames) under every store mode
     (1, 5, 2, 0, 1), (1, 5, 2, 0, 9), (1, 5, 2, 0, 5), (1, 5, 2, 0, 2), (1, 5, 2, 0, 0),
     # the zero-copy host path's small-batch group shapes
@@ -315,8 +317,9 @@ def test_every_launch_shape_is_bit_exact(dev, shape, layout):
     assert np.array_equal(umem.cpu().numpy(), ou)
 
 
-@pytest.mark.parametrize("shape", [(32, 3, 2, 0), (64, 2, 4, 0), (16, 3, 1, 0, 0, 1, 24), (16, 2, 2, 0, 0, 1, 20)],
-                         ids=["reg32", "reg64", "split-w8", "split-w4"])
+@pytest.mark.parametrize("shape", [(32, 3, 2, 0), (64, 2, 4, 0), (16, 3, 1, 0, 0, 1, 24), (16, 2, 2, 0, 0, 1, 20),
+                                   (16, 2, 2, 0, 0, 1, 56)],
+                         ids=["reg32", "reg64", "split-w8", "split-w4", "split-pool"])
 def test_records_only_mode(dev, shape):
     """fused_stores = 3: the UMEM is only read; applying the records as
     include/xsknf_gpu.h documents them gives the oracle's bytes and verdicts."""
@@ -472,7 +475,7 @@ def test_concurrent_streams(dev):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 24),
+@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 24), (16, 2, 2, 0, 18, 1, 56),
                                    pytest.param((16, 3, 2, 0, 18, 1, 24),
                                                 marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only"))],
                          ids=_shape_id)

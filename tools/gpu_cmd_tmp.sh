@@ -1,7 +1,5 @@
 set -o pipefail
-mkdir -p gpurun_out/nch
-for rep in 1 2 3; do
-for W in 1500 1024 800; do
-  timeout -k 10 120 python tools/tune.py --workload $W --bpc 4 --rounds 5 --variants 16,3,2,0,18,1,24 >> gpurun_out/nch/res.jsonl 2>>gpurun_out/nch/err || exit 1
-done; done
-cut -c1-140 gpurun_out/nch/res.jsonl
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pool_tests.log 2>&1; rc=$?; tail -3 gpurun_out/pool_tests.log
+[ $rc = 0 ] || { grep -E "FAILED|Error" gpurun_out/pool_tests.log | head; exit 1; }
+VARIANTS=16,2,2,0,18,1,56 bash tools/ab_dyn.sh pool1 xsknf_amd/lib || exit 1
+bash tools/timeline.sh tl7 1500:16,2,2,0,18,1,56 570:16,2,2,0,18,1,56 imix:16,2,2,0,18,1,56

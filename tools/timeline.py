@@ -86,7 +86,24 @@ def main():
         torch.cuda.synchronize()
         _lib.check(lib.xsknf_gpu_ab_set_timeline(None), "timeline off")
         t = tl.view(-1, 8).cpu().numpy()
+        gw = np.nonzero(t[:, 0] != 0)[0]
         t = t[t[:, 0] != 0]
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        wpb = 12 if cfg.window_chunks & 32 else 4   # waves per block (window + 32: one 12-wave block per CU)
+        bslot, xcd, wvi = (gw // wpb) // cus, (gw // wpb) % 8, gw % 4
+        blk = gw // wpb
+        sd_us = (t[:, 1] - t[:, 0].min()) / 100.0
+        nb = int(blk.max()) + 1
+        bmax = np.full(nb, -1e9); bmin = np.full(nb, 1e9); bsum = np.zeros(nb); bcnt = np.zeros(nb)
+        np.maximum.at(bmax, blk, sd_us); np.minimum.at(bmin, blk, sd_us)
+        np.add.at(bsum, blk, sd_us); np.add.at(bcnt, blk, 1)
+        ok = bcnt > 0
+        bspread = (bmax - bmin)[ok]
+        bmean = (bsum / np.maximum(bcnt, 1))[ok]
+        cu = blk % cus
+        csum = np.zeros(cus); ccnt = np.zeros(cus)
+        np.add.at(csum, cu, sd_us); np.add.at(ccnt, cu, 1)
+        cmean = (csum / np.maximum(ccnt, 1))[ccnt > 0]
         t0 = t[:, 0].min()
         start, sdone, pdone = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, (t[:, 2] - t0) / 100.0   # us
         end = pdone.max()
@@ -105,6 +122,16 @@ def main():
             "tiles": {int(k): int(v) for k, v in zip(*np.unique(tiles, return_counts=True))},
             "per_wave_us_phaseA_window_parse_B": [round(float(t[:, k].mean()) / 100.0, 2) for k in (4, 5, 6)],
             "stream_done_by_tiles": {int(k): pct(sdone[tiles == k], 50) for k in np.unique(tiles)},
+            # wave index = block * 4 + wave: block slot on its CU (dispatch order) and XCD (block % 8)
+            "stream_done_p50_max_by_block_slot": {int(b): [pct(sdone[bslot == b], 50), pct(sdone[bslot == b], 100)]
+                                                  for b in np.unique(bslot)},
+            "stream_done_p50_max_by_xcd": {int(x): [pct(sdone[xcd == x], 50), pct(sdone[xcd == x], 100)]
+                                           for x in np.unique(xcd)},
+            "stream_done_p50_by_simd": {int(w): pct(sdone[wvi == w], 50) for w in range(4)},
+            # pooling potential: a block's 4 waves sharing their tiles would end near their mean
+            "block_internal_spread_p50_p90": [pct(bspread, 50), pct(bspread, 90)],
+            "stream_end_if_pooled_per_block": pct(bmean, 100),
+            "stream_end_if_pooled_per_cu": pct(cmean, 100),
         })
     rows.sort(key=lambda x: x["kernel_us"])
     med = rows[len(rows) // 2]

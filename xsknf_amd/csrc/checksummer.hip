@@ -1216,11 +1216,13 @@ __device__ __forceinline__ void timeline_put(uint32_t wave, int lane, unsigned l
 }
 #endif
 
+constexpr uint32_t kNoTile = 0xffffffffu;
+
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
 // +8-11 % from 2 -> 3 waves per SIMD, so the register budget is pinned.
-template <int W, int LPF, int NCH, int U, bool TL, bool DMA, bool PFW>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U == 1 || DMA ? 4 : 1)))
+template <int W, int LPF, int NCH, int U, bool TL, bool DMA, bool PFW, int SW>
+__global__ __launch_bounds__(SW * kWave) __attribute__((amdgpu_waves_per_eu(U == 1 || DMA ? 4 : 1)))
 void checksum_kernel_split(const KernelArgs args) {
   static_assert(W >= 4 && (W <= kHdrChunks || W == 8), "header window");
   static_assert(!PFW || (TL && !DMA && W == 8), "window prefetch: the transposed W = 8 layout, register phase B");
@@ -1232,14 +1234,15 @@ void checksum_kernel_split(const KernelArgs args) {
   constexpr int kSlotArea = kWave * kSlot;                 // bytes per wave
   constexpr int kItemCap = 256;                            // items per round of phase B
   constexpr uint32_t kItemsPerFrame = 255;                 // u8 pass index; more: whole-wave loop
-  __shared__ __attribute__((aligned(16))) uint8_t slots[kWavesPerBlock][kSlotArea];
-  __shared__ __attribute__((aligned(16))) uint16_t itemq[kWavesPerBlock][kItemCap];
-  __shared__ __attribute__((aligned(16))) uint4 meta[kWavesPerBlock][kWave];
-  __shared__ __attribute__((aligned(16))) uint32_t accb[kWavesPerBlock][kWave];
+  __shared__ __attribute__((aligned(16))) uint8_t slots[SW][kSlotArea];
+  __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kItemCap];
+  __shared__ __attribute__((aligned(16))) uint4 meta[SW][kWave];
+  __shared__ __attribute__((aligned(16))) uint32_t accb[SW][kWave];
   // patch list tiles: 16 x 2 items fit 3 waves per SIMD (6 tiles per wave at 1M
   // frames), 16 x 3 fit 2 (8 tiles per wave)
-  constexpr int PT = (W == 8 && U == 2 && !DMA && !PFW) ? (NCH == 2 ? kPatchTiles : 8) : 0;
-  __shared__ __attribute__((aligned(16))) uint2 plist[kWavesPerBlock][PT > 0 ? PT * kWave : 1];
+  constexpr bool kPool = SW > kWavesPerBlock;   // one block per CU: its waves share the CU's tiles
+  constexpr int PT = (W == 8 && U == 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
+  __shared__ __attribute__((aligned(16))) uint2 plist[SW][PT > 0 ? PT * kWave : 1];
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1249,10 +1252,9 @@ void checksum_kernel_split(const KernelArgs args) {
   const uint32_t mt = lds_addr(&meta[wv][0]);
   const uint32_t ab = lds_addr(&accb[wv][0]);
   const uint32_t iq = lds_addr(&itemq[wv][0]);
-  const uint32_t waves = gridDim.x * kWavesPerBlock;
+  const uint32_t waves = gridDim.x * SW;
   const uint32_t last = args.n - 1;
 
-  uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
   uint32_t nrec = 0;
 #ifdef XSKNF_TIMELINE
   const unsigned long long tl0 = wall_clock64();
@@ -1267,9 +1269,43 @@ void checksum_kernel_split(const KernelArgs args) {
   const bool list_ok = PT > 0 && args.tail_scatter && args.umem_size < kPatchMaxUmem;
   int it = 0;              // tiles done by this wave
   bool any_entry = false;  // wave-uniform: the patch list holds an entry
+  // The wave's tiles: `tile`, then `tn`, `tnn` (kNoTile: none).
+  // * SW = 4 (several blocks per CU): every waves-th tile from the wave's index.
+  // * kPool (SW = 12: one block holds every wave of its CU): the block's tiles,
+  //   every nb-th from the block index, are a pool its waves draw from -- the
+  //   first three rounds by wave index, then through an LDS counter, three tiles
+  //   ahead.  A CU's waves do not stream equally fast: with three 4-wave blocks
+  //   per CU the third block's waves ended their streams ~40 us after the first
+  //   two's at 1500 B, and the launch waits for the last one
+  //   (tools/timeline.py); from a shared pool the faster waves take more tiles.
+  //   A tile past the wave's patch list writes its checks in-line.  (A global
+  //   counter was tried: its atomics retire in vmcnt order, and each round trip
+  //   held up the next load wait -- 1500 B 347 vs 291 us.)
+  const uint32_t ntiles = (args.n + kWave - 1) / kWave;
+  __shared__ uint32_t pool_next;
+  const uint32_t nb = gridDim.x;
+  const uint32_t bt = ntiles > blockIdx.x ? (ntiles - blockIdx.x + nb - 1) / nb : 0u;   // the block's tiles
+  const auto pool_tile = [&](uint32_t p) { return p < bt ? blockIdx.x + p * nb : kNoTile; };
+  bool pool_live = kPool;   // wave-uniform: no failed dequeue yet
+  uint32_t tile, tn, tnn;
+  if constexpr (kPool) {
+    tile = pool_tile(wv);
+    tn = pool_tile(wv + SW);
+    tnn = pool_tile(wv + 2 * SW);
+    if (threadIdx.x == 0) pool_next = 3 * SW;
+    __syncthreads();
+  } else {
+    const uint32_t t0 = blockIdx.x * SW + wv;
+    tile = t0 < ntiles ? t0 : kNoTile;
+    tn = t0 + waves < ntiles ? t0 + waves : kNoTile;
+    tnn = t0 + 2 * waves < ntiles ? t0 + 2 * waves : kNoTile;
+  }
+  const auto desc_of = [&](uint32_t t) {
+    return *reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(t * kWave + lane, last)));
+  };
   // descriptors travel two tiles ahead
-  uint4 d = *reinterpret_cast<const uint4 *>(args.descs + min(tile * kWave + lane, last));
-  uint4 dn = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * kWave + lane, last));
+  uint4 d = desc_of(tile);
+  uint4 dn = desc_of(tn);
   // PFW: the next tile's header windows go straight into the slots by LDS-DMA
   // as soon as this tile's phase A is done with them (every check deferred: the
   // slots are dead until then), so a tile starts on windows already in LDS.
@@ -1295,8 +1331,11 @@ void checksum_kernel_split(const KernelArgs args) {
     window_dma(d, tile * kWave + lane);
     window_pending = true;
   }
-  for (; tile * kWave < args.n; tile += waves) {
+  while (tile != kNoTile) {
     XSKNF_TL_START();
+    uint32_t dq = 0;   // the pool index of the tile three ahead, back by the end of this tile
+    if constexpr (kPool)
+      if (pool_live && lane == 0) dq = __hip_atomic_fetch_add(&pool_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t f = tile * kWave + lane;
     const FrameRef r = lane_ref(args, d, f);
     uint4 v[W];
@@ -1331,10 +1370,12 @@ void checksum_kernel_split(const KernelArgs args) {
       load_lane<W>(r, v);
     }
     XSKNF_TL_MARK(tl_a);
-    const uint4 dnn = *reinterpret_cast<const uint4 *>(args.descs + min((tile + 2 * waves) * kWave + lane, last));
+    const uint4 dnn = desc_of(tnn);
+    const bool to_list = list_ok && it < PT;   // wave-uniform
     // per-tile store policy, as the register kernel: long frames defer their
     // checks only where they are at least half of the tile
-    uint32_t defer_min = args.defer_min_len;
+    // (a pooled wave's tiles past its list: in-line; the record path walks the static schedule)
+    uint32_t defer_min = kPool && args.tail_scatter && !to_list ? kNoDefer : args.defer_min_len;
     if (defer_min != kNoDefer && defer_min != 0 && !args.no_scatter) {
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(f < args.n && d.z >= defer_min)));
@@ -1371,7 +1412,6 @@ void checksum_kernel_split(const KernelArgs args) {
     const bool huge = items > kItemsPerFrame;
     int32_t res = r.exists ? verdict : 0;
     LaneOut o = {res, false, slot, r.fp};
-    const bool to_list = list_ok && it < PT;   // wave-uniform
     uint2 ent = make_uint2(0, 0);
     if (do_sum && !more) {
       const uint16_t c = check_of(h, PA, args.payload_mult);
@@ -1399,8 +1439,8 @@ void checksum_kernel_split(const KernelArgs args) {
     store_sectors(o, lane, args.plain_sector);
     const uint32_t part = h.pseudo + args.payload_mult * (PA - h.old_check);
     if constexpr (PFW) {
-      window_pending = (tile + waves) * kWave < args.n;
-      if (window_pending) window_dma(dn, (tile + waves) * kWave + lane);
+      window_pending = tn != kNoTile;
+      if (window_pending) window_dma(dn, tn * kWave + lane);
     }
 
     // ---- phase B: payload items of the longer frames ----
@@ -1494,6 +1534,18 @@ void checksum_kernel_split(const KernelArgs args) {
     }
     ++it;
     compiler_barrier();   // the next tile rewrites the slots
+    uint32_t t3 = kNoTile;
+    if constexpr (kPool) {
+      if (pool_live) {
+        t3 = pool_tile(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dq), 0)));
+        pool_live = t3 != kNoTile;
+      }
+    } else if (tnn != kNoTile && tnn + waves < ntiles) {
+      t3 = tnn + waves;
+    }
+    tile = tn;
+    tn = tnn;
+    tnn = t3;
     d = dn;
     dn = dnn;
   }
@@ -1504,13 +1556,13 @@ void checksum_kernel_split(const KernelArgs args) {
   if (args.tail_scatter) {
     if (any_entry) tail_patch_list(args, pl, min(it, PT), lane, it <= PT, area, kSlot);
     if (__builtin_amdgcn_readfirstlane(nrec))
-      tail_scatter(args, blockIdx.x * kWavesPerBlock + wv + (list_ok ? PT : 0) * waves, waves, lane);
+      tail_scatter(args, blockIdx.x * SW + wv + (list_ok ? PT : 0) * waves, waves, lane);   // static schedule only
   } else {
     publish_records(args, nrec, lane);
   }
 #ifdef XSKNF_TIMELINE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  timeline_put(blockIdx.x * kWavesPerBlock + wv, lane, tl0, tl1, it, tl_a, tl_p, tl_b);
+  timeline_put(blockIdx.x * SW + wv, lane, tl0, tl1, it, tl_a, tl_p, tl_b);
 #endif
 }
 
@@ -1819,7 +1871,7 @@ int device_cus() {
 // resident at once (occupancy by VGPR / LDS of the instantiation), capped by
 // blocks_per_cu.  A grid larger than residency would run in rounds with an
 // idle tail, since tiles are dealt to waves statically.
-int resident_blocks(const void *kernel) {
+int resident_blocks(const void *kernel, int threads) {
   struct Entry { const void *k; int dev; int blocks; };
   static thread_local Entry cache[64];
   static thread_local int used = 0;
@@ -1828,17 +1880,17 @@ int resident_blocks(const void *kernel) {
   for (int i = 0; i < used; ++i)
     if (cache[i].k == kernel && cache[i].dev == dev) return cache[i].blocks;
   int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kBlock, 0) != hipSuccess || b <= 0) b = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, threads, 0) != hipSuccess || b <= 0) b = 1;
   if (used < 64) cache[used++] = Entry{kernel, dev, b};
   return b;
 }
 
 template <typename K>
-uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_frames) {
-  const int resident = resident_blocks(reinterpret_cast<const void *>(kernel));
+uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_frames, int waves_per_block = kWavesPerBlock) {
+  const int resident = resident_blocks(reinterpret_cast<const void *>(kernel), waves_per_block * kWave);
   const int per_cu = blocks_per_cu < resident ? blocks_per_cu : resident;
   const uint32_t tiles = (n + tile_frames - 1) / tile_frames;
-  const uint32_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint32_t need = (tiles + waves_per_block - 1) / waves_per_block;
   const uint32_t cap = static_cast<uint32_t>(device_cus() * per_cu);
   return need < cap ? need : cap;
 }
@@ -1875,12 +1927,12 @@ int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
 
-template <int W, int LPF, int NCH, int U, bool TL, bool DMA, bool PFW = false>
+template <int W, int LPF, int NCH, int U, bool TL, bool DMA, bool PFW = false, int SW = kWavesPerBlock>
 int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   // the DMA stages / the window prefetch reuse the windows: every check deferred
   if ((DMA || PFW) && a.defer_min_len != 0) return -EINVAL;
-  auto k = checksum_kernel_split<W, LPF, NCH, U, TL, DMA, PFW>;
-  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave)), dim3(kBlock), 0, stream, a);
+  auto k = checksum_kernel_split<W, LPF, NCH, U, TL, DMA, PFW, SW>;
+  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave, SW)), dim3(SW * kWave), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_split launch");
 }
 
@@ -1911,9 +1963,12 @@ struct Variant {
 #define XSKNF_SD(W, L, N, U) {L, N, U, 1, &launch_split<W, L, N, U, true, true>, XSKNF_GPU_KERNEL_SPLIT, W + 16}
 // header windows prefetched by LDS-DMA one tile ahead (lds_ring field = 2); every check deferred
 #define XSKNF_SP(L, N, U) {L, N, U, 2, &launch_split<8, L, N, U, true, false, true>, XSKNF_GPU_KERNEL_SPLIT, 24}
+// one 12-wave block per CU, its waves drawing the CU's tiles from a shared pool (window field + 32)
+#define XSKNF_SC(L, N, U) {L, N, U, 0, &launch_split<8, L, N, U, true, false, false, 12>, XSKNF_GPU_KERNEL_SPLIT, 56}
 const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
-    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_S(8, 16, 3, 1, 1), XSKNF_S(4, 16, 3, 2, 1),
+    XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_SC(16, 2, 2), XSKNF_S(8, 16, 3, 1, 1),
+    XSKNF_S(4, 16, 3, 2, 1),
     // ... the lane kernel for short frames ...
     XSKNF_L(5, 2),
     // ... and the zero-copy host path's small-batch group shapes (host_path.hip)
@@ -1945,6 +2000,7 @@ const Variant kVariants[] = {
 #undef XSKNF_S
 #undef XSKNF_SD
 #undef XSKNF_SP
+#undef XSKNF_SC
 
 const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   for (const Variant &v : kVariants) {
@@ -1986,7 +2042,10 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   //    tile, two tiles' patches in flight (no second launch): 570 B 148.8 us
   //    [in-line 170.2], IMIX 117.8 [per-tile policy + scatter pass 125-136,
   //    all in-line 127], 1500 B 291.6-292.5 [16 x 3 items + scatter pass
-  //    294.4-297.4];
+  //    294.4-297.4]; one 12-wave block per CU whose waves share the CU's
+  //    tiles (window + 32), same process, interleaved: 1500 B 283.4 vs 292.6,
+  //    1024 B 201.5 vs 206.8, 570 B 148.7 vs 150.1, IMIX 115.8 vs 114.8
+  //    (profiles/r02/ab_pool.jsonl);
   //  * jumbo: 4-chunk window, 16 x 3 items, two per group in flight, the
   //    per-tile policy + scatter pass: 9000 B 1467 us [tail patches 1491].
   c.kernel = XSKNF_GPU_KERNEL_SPLIT;
@@ -1996,7 +2055,7 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
     c.lanes_per_frame = 1; c.window_chunks = 0; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
   } else if (hint + 15 <= 4096) {
     (void)mean;
-    c.window_chunks = 8 + 16; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
+    c.window_chunks = 8 + 16 + 32; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   } else {
     c.window_chunks = 4 + 16; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
   }
