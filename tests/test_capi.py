@@ -99,8 +99,9 @@ def test_ctx_argument_validation_without_gpu():
 
 def test_launch_shape_for_lengths_without_gpu():
     """xsknf_gpu_launch_cfg_for_lens: the largest frame picks the kernel family
-    and the header window; the mean length does not change the product's shape
-    (the long-frame 16 x 3 items are an A/B shape)."""
+    and the header window; for <= 4 KiB frames the mean picks the CU-wide tile
+    pool (window + 32; also for an unknown mean) or, for a mix of mostly short
+    frames (mean < 512), 4-wave blocks with the static schedule."""
     lib = _lib.load()
 
     def shape(mx, mean):
@@ -110,11 +111,11 @@ def test_launch_shape_for_lengths_without_gpu():
 
     plain = _lib.LaunchCfg()
     assert lib.xsknf_gpu_default_launch_cfg(1500, ctypes.byref(plain)) == 0
-    for mean in (0, 352, 1023, 1280, 1500):
+    for mean in (0, 512, 1023, 1500):
         assert shape(1500, mean) == (plain.kernel, plain.lanes_per_frame, plain.chunks_per_lane,
                                      plain.window_chunks, plain.fused_stores)
     assert shape(1500, 1500)[2] == 2 and shape(1500, 1500)[3] == 56
-    assert shape(4000, 1024)[2] == 2 and shape(4000, 1280)[2] == 2
+    assert shape(1500, 352)[3] == 24 and shape(1500, 511)[3] == 24 and shape(4000, 1024)[3] == 56
     assert shape(9000, 9000)[3] == 20          # jumbo: 4-chunk window, whatever the mean
     assert shape(64, 64)[1] == 1               # lane kernel
     assert lib.xsknf_gpu_launch_cfg_for_lens(1500, 1500, None) == -errno.EINVAL

@@ -1285,14 +1285,35 @@ void checksum_kernel_split(const KernelArgs args) {
   __shared__ uint32_t pool_next;
   const uint32_t nb = gridDim.x;
   const uint32_t bt = ntiles > blockIdx.x ? (ntiles - blockIdx.x + nb - 1) / nb : 0u;   // the block's tiles
-  const auto pool_tile = [&](uint32_t p) { return p < bt ? blockIdx.x + p * nb : kNoTile; };
+  // The pool's units: the block's tiles, except that its last SW tiles run as
+  // two 32-frame halves each, so the waves' streams end within half a tile of
+  // each other (whole tiles: 46 us apart at 1500 B, one tile's time).
+  const uint32_t nsplit = kPool ? min(bt, static_cast<uint32_t>(SW)) : 0u;
+  const uint32_t nfull = bt - nsplit;
+  const uint32_t units = nfull + 2 * nsplit;
+  const auto pool_unit = [&](uint32_t p) { return p < units ? p : kNoTile; };
+  // first frame and frame count of unit / static tile u
+  const auto unit_f0 = [&](uint32_t u) -> uint32_t {
+    if constexpr (kPool) {
+      if (u < nfull) return (blockIdx.x + u * nb) * kWave;
+      const uint32_t h = u - nfull;
+      return (blockIdx.x + (nfull + h / 2) * nb) * kWave + (h & 1) * (kWave / 2);
+    } else {
+      return u * kWave;
+    }
+  };
+  const auto unit_cnt = [&](uint32_t u) -> uint32_t { return kPool && u >= nfull ? kWave / 2 : kWave; };
   bool pool_live = kPool;   // wave-uniform: no failed dequeue yet
-  uint32_t tile, tn, tnn;
+  uint32_t tile, tn, tnn;   // pool units (kPool) or tiles
   if constexpr (kPool) {
-    tile = pool_tile(wv);
-    tn = pool_tile(wv + SW);
-    tnn = pool_tile(wv + 2 * SW);
-    if (threadIdx.x == 0) pool_next = 3 * SW;
+    // one unit ahead only: a wave holds at most the unit it sums and the next
+    // (three ahead, the waves of a block ended 43 us apart at 1500 B: 284.5 vs
+    // 279.2 us; claiming when the unit's payload starts instead of at its
+    // start: 1500 B a tie, 570 B 149.1 vs 146.7, IMIX 118.5 vs 115.9 --
+    // profiles/r02/ab_pool.jsonl)
+    tile = pool_unit(wv);
+    tn = tnn = kNoTile;
+    if (threadIdx.x == 0) pool_next = SW;
     __syncthreads();
   } else {
     const uint32_t t0 = blockIdx.x * SW + wv;
@@ -1301,11 +1322,11 @@ void checksum_kernel_split(const KernelArgs args) {
     tnn = t0 + 2 * waves < ntiles ? t0 + 2 * waves : kNoTile;
   }
   const auto desc_of = [&](uint32_t t) {
-    return *reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(t * kWave + lane, last)));
+    return *reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(unit_f0(t) + lane, last)));
   };
-  // descriptors travel two tiles ahead
+  // descriptors travel two tiles ahead (static), one unit ahead (kPool)
   uint4 d = desc_of(tile);
-  uint4 dn = desc_of(tn);
+  uint4 dn = kPool ? d : desc_of(tn);
   // PFW: the next tile's header windows go straight into the slots by LDS-DMA
   // as soon as this tile's phase A is done with them (every check deferred: the
   // slots are dead until then), so a tile starts on windows already in LDS.
@@ -1328,15 +1349,21 @@ void checksum_kernel_split(const KernelArgs args) {
   bool window_pending = false;
   if constexpr (PFW) {
     static_assert(!PFW || kSlot == 16 * W, "DMA layout = slot layout");
-    window_dma(d, tile * kWave + lane);
+    window_dma(d, unit_f0(tile) + lane);
     window_pending = true;
   }
   while (tile != kNoTile) {
     XSKNF_TL_START();
-    uint32_t dq = 0;   // the pool index of the tile three ahead, back by the end of this tile
-    if constexpr (kPool)
+    if constexpr (kPool) {   // claim the next unit, and load its descriptors while this one streams
+      uint32_t dq = 0;
       if (pool_live && lane == 0) dq = __hip_atomic_fetch_add(&pool_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint32_t f = tile * kWave + lane;
+      tn = pool_live ? pool_unit(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dq), 0))) : kNoTile;
+      pool_live = tn != kNoTile;
+      dn = desc_of(tn);
+    }
+
+    const uint32_t f0 = unit_f0(tile), cnt = unit_cnt(tile);
+    const uint32_t f = lane < cnt ? f0 + lane : args.n;   // lanes past a half unit hold no frame
     const FrameRef r = lane_ref(args, d, f);
     uint4 v[W];
     if constexpr (PFW) {
@@ -1370,7 +1397,7 @@ void checksum_kernel_split(const KernelArgs args) {
       load_lane<W>(r, v);
     }
     XSKNF_TL_MARK(tl_a);
-    const uint4 dnn = desc_of(tnn);
+    const uint4 dnn = kPool ? d : desc_of(tnn);
     const bool to_list = list_ok && it < PT;   // wave-uniform
     // per-tile store policy, as the register kernel: long frames defer their
     // checks only where they are at least half of the tile
@@ -1379,7 +1406,7 @@ void checksum_kernel_split(const KernelArgs args) {
     if (defer_min != kNoDefer && defer_min != 0 && !args.no_scatter) {
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(f < args.n && d.z >= defer_min)));
-      const uint32_t nlive = min(static_cast<uint32_t>(kWave), args.n - tile * kWave);
+      const uint32_t nlive = f0 < args.n ? min(cnt, args.n - f0) : 0u;
       if (XSKNF_DEFER_TILE_K > 0 && XSKNF_DEFER_TILE_K * nlong < nlive) defer_min = kNoDefer;
     }
 
@@ -1440,7 +1467,7 @@ void checksum_kernel_split(const KernelArgs args) {
     const uint32_t part = h.pseudo + args.payload_mult * (PA - h.old_check);
     if constexpr (PFW) {
       window_pending = tn != kNoTile;
-      if (window_pending) window_dma(dn, tn * kWave + lane);
+      if (window_pending) window_dma(dn, unit_f0(tn) + lane);
     }
 
     // ---- phase B: payload items of the longer frames ----
@@ -1534,20 +1561,17 @@ void checksum_kernel_split(const KernelArgs args) {
     }
     ++it;
     compiler_barrier();   // the next tile rewrites the slots
-    uint32_t t3 = kNoTile;
     if constexpr (kPool) {
-      if (pool_live) {
-        t3 = pool_tile(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dq), 0)));
-        pool_live = t3 != kNoTile;
-      }
-    } else if (tnn != kNoTile && tnn + waves < ntiles) {
-      t3 = tnn + waves;
+      tile = tn;
+      d = dn;
+    } else {
+      const uint32_t t3 = tnn != kNoTile && tnn + waves < ntiles ? tnn + waves : kNoTile;
+      tile = tn;
+      tn = tnn;
+      tnn = t3;
+      d = dn;
+      dn = dnn;
     }
-    tile = tn;
-    tn = tnn;
-    tnn = t3;
-    d = dn;
-    dn = dnn;
   }
 #ifdef XSKNF_TIMELINE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2017,13 +2041,15 @@ const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   return nullptr;
 }
 
-// The mean length does not change the product's shape today.  16 x 3 items
-// (two in flight, 188 VGPRs: 2 waves per SIMD, 8 tiles per wave at 1M frames)
-// for batches of mean >= 1280 B measured 1500 B 283.0 vs 287.7 us, 288.2-296.9
-// vs 290.7-302.6 (profiles/r02/ab_nch3.jsonl, ab_nch3_lengths.jsonl), but one
-// launch of it over a batch larger than its patch lists (one block per CU)
-// faulted once in the full GPU suite and could not be reproduced alone, so it
-// stays an A/B shape.
+// Mean frame length under which a batch of <= 4 KiB frames keeps 4-wave blocks
+// and the static schedule (0 = unknown: the CU-wide pool).  16 x 3 items (two
+// in flight, 188 VGPRs: 2 waves per SIMD) for batches of mean >= 1280 B
+// measured 1500 B 283.0 vs 287.7 us against 4-wave 16 x 2 (profiles/r02/
+// ab_nch3.jsonl), but one launch of it over a batch larger than its patch
+// lists faulted once in the full GPU suite and could not be reproduced alone,
+// so it stays an A/B shape.
+constexpr uint32_t kPoolMinMean = 512;
+
 // Default shape for a batch whose longest frame is `hint` bytes and whose
 // mean length is `mean` (0 = unknown: the shape that suits any mix).
 void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
@@ -2054,8 +2080,10 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
     c.kernel = XSKNF_GPU_KERNEL_AUTO;
     c.lanes_per_frame = 1; c.window_chunks = 0; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
   } else if (hint + 15 <= 4096) {
-    (void)mean;
-    c.window_chunks = 8 + 16 + 32; c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
+    // the CU-wide tile pool (+ 32) but for a known mix of mostly short frames
+    // (IMIX: 115.9 vs 114.3 us with 4-wave blocks and the static schedule)
+    c.window_chunks = 8 + 16 + (mean != 0 && mean < kPoolMinMean ? 0 : 32);
+    c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   } else {
     c.window_chunks = 4 + 16; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
   }
