@@ -1288,30 +1288,25 @@ void checksum_kernel_split(const KernelArgs args) {
   // The pool's units: the block's tiles, except that its last SW tiles run as
   // two 32-frame halves each, so the waves' streams end within half a tile of
   // each other (whole tiles: 46 us apart at 1500 B, one tile's time).
-#ifndef XSKNF_POOL_QUARTERS
-#define XSKNF_POOL_QUARTERS 0
+#ifndef XSKNF_POOL_HALVES
+#define XSKNF_POOL_HALVES 1
 #endif
-  // (A/B, XSKNF_POOL_QUARTERS: the very last SW tiles as four 16-frame quarters, the SW before as halves)
-  const uint32_t nq = kPool && XSKNF_POOL_QUARTERS ? min(bt, static_cast<uint32_t>(SW)) : 0u;
-  const uint32_t nsplit = kPool ? min(bt - nq, static_cast<uint32_t>(SW)) : 0u;
-  const uint32_t nfull = bt - nq - nsplit;
-  const uint32_t units = nfull + 2 * nsplit + 4 * nq;
+  // (16-frame quarters for the last SW tiles, A/B: 570 B 165 vs 151 us, 1024 B 213 vs 205 -- ab_pool.jsonl)
+  const uint32_t nsplit = kPool && XSKNF_POOL_HALVES ? min(bt, static_cast<uint32_t>(SW)) : 0u;
+  const uint32_t nfull = bt - nsplit;
+  const uint32_t units = nfull + 2 * nsplit;
   const auto pool_unit = [&](uint32_t p) { return p < units ? p : kNoTile; };
   // first frame and frame count of unit / static tile u
   const auto unit_f0 = [&](uint32_t u) -> uint32_t {
     if constexpr (kPool) {
       if (u < nfull) return (blockIdx.x + u * nb) * kWave;
       const uint32_t h = u - nfull;
-      if (h < 2 * nsplit) return (blockIdx.x + (nfull + h / 2) * nb) * kWave + (h & 1) * (kWave / 2);
-      const uint32_t q = h - 2 * nsplit;
-      return (blockIdx.x + (nfull + nsplit + q / 4) * nb) * kWave + (q & 3) * (kWave / 4);
+      return (blockIdx.x + (nfull + h / 2) * nb) * kWave + (h & 1) * (kWave / 2);
     } else {
       return u * kWave;
     }
   };
-  const auto unit_cnt = [&](uint32_t u) -> uint32_t {
-    return !kPool || u < nfull ? kWave : (u < nfull + 2 * nsplit ? kWave / 2 : kWave / 4);
-  };
+  const auto unit_cnt = [&](uint32_t u) -> uint32_t { return kPool && u >= nfull ? kWave / 2 : kWave; };
   bool pool_live = kPool;   // wave-uniform: no failed dequeue yet
   uint32_t tile, tn, tnn;   // pool units (kPool) or tiles
   if constexpr (kPool) {
