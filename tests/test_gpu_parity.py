@@ -249,6 +249,8 @@ PRODUCT_SHAPES = [
     (16, 3, 2, 0, 0, 1, 20), (16, 3, 2, 0, 2, 1, 20), (16, 3, 2, 0, 20, 1, 20), (16, 3, 2, 0, 1, 1, 20),
     # one 12-wave block per CU sharing the CU's tiles (window + 32)
     (16, 2, 2, 0, 18, 1, 56), (16, 2, 2, 0, 2, 1, 56), (16, 2, 2, 0, 0, 1, 56), (16, 2, 2, 0, 1, 1, 56),
+    # jumbo: one 8-wave block per CU sharing the CU's tiles, 16-frame quarters at the end
+    (16, 3, 2, 0, 0, 1, 52), (16, 3, 2, 0, 1, 1, 52), (16, 3, 2, 0, 2, 1, 52), (16, 3, 2, 0, 18, 1, 52),
     # the lane kernel (short frames) under every store mode
     (1, 5, 2, 0, 1), (1, 5, 2, 0, 9), (1, 5, 2, 0, 5), (1, 5, 2, 0, 2), (1, 5, 2, 0, 0),
     # the zero-copy host path's small-batch group shapes
@@ -268,6 +270,7 @@ AB_SHAPES = [
     (16, 2, 1, 0, 5, 1, 20), (16, 3, 1, 0, 1, 1, 20), (16, 2, 1, 0, 1, 1, 24), (32, 3, 1, 0, 2, 1, 24),
     # 16 x 3 items with the 8-tile patch list (long-frame batches, not in the product)
     (16, 3, 2, 0, 18, 1, 24), (16, 3, 2, 0, 2, 1, 24), (16, 3, 2, 0, 0, 1, 24), (16, 3, 2, 0, 1, 1, 24),
+    (16, 3, 2, 0, 0, 1, 116), (16, 3, 2, 0, 18, 1, 116),
     # split kernel with LDS-DMA phase B (ring 1) / window prefetch (ring 2): every check deferred only
     (16, 2, 2, 1, 18, 1, 24), (16, 4, 1, 1, 2, 1, 24), (16, 2, 2, 2, 18, 1, 24), (16, 3, 1, 2, 2, 1, 24),
 ]
@@ -318,8 +321,8 @@ def test_every_launch_shape_is_bit_exact(dev, shape, layout):
 
 
 @pytest.mark.parametrize("shape", [(32, 3, 2, 0), (64, 2, 4, 0), (16, 3, 1, 0, 0, 1, 24), (16, 2, 2, 0, 0, 1, 20),
-                                   (16, 2, 2, 0, 0, 1, 56)],
-                         ids=["reg32", "reg64", "split-w8", "split-w4", "split-pool"])
+                                   (16, 2, 2, 0, 0, 1, 56), (16, 3, 2, 0, 0, 1, 52)],
+                         ids=["reg32", "reg64", "split-w8", "split-w4", "split-pool", "split-w4-pool"])
 def test_records_only_mode(dev, shape):
     """fused_stores = 3: the UMEM is only read; applying the records as
     include/xsknf_gpu.h documents them gives the oracle's bytes and verdicts."""

@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 from xsknf_amd import _lib, frames  # noqa: E402
 
 WL = {"1500": (1500, "aligned"), "imix": ("imix", "aligned"), "570": (570, "aligned"),
-      "1024": (1024, "aligned")}
+      "1024": (1024, "aligned"), "jumbo": (9000, "unaligned")}
 
 
 def pct(x, q):

@@ -1292,21 +1292,23 @@ void checksum_kernel_split(const KernelArgs args) {
 #define XSKNF_POOL_HALVES 1
 #endif
   // (16-frame quarters for the last SW tiles, A/B: 570 B 165 vs 151 us, 1024 B 213 vs 205 -- ab_pool.jsonl)
+  // jumbo tiles (W = 4) end in quarters: a 64-frame tile of 9000 B frames streams for ~160 us
+  constexpr uint32_t kParts = W == 4 ? 4u : 2u;
   const uint32_t nsplit = kPool && XSKNF_POOL_HALVES ? min(bt, static_cast<uint32_t>(SW)) : 0u;
   const uint32_t nfull = bt - nsplit;
-  const uint32_t units = nfull + 2 * nsplit;
+  const uint32_t units = nfull + kParts * nsplit;
   const auto pool_unit = [&](uint32_t p) { return p < units ? p : kNoTile; };
   // first frame and frame count of unit / static tile u
   const auto unit_f0 = [&](uint32_t u) -> uint32_t {
     if constexpr (kPool) {
       if (u < nfull) return (blockIdx.x + u * nb) * kWave;
       const uint32_t h = u - nfull;
-      return (blockIdx.x + (nfull + h / 2) * nb) * kWave + (h & 1) * (kWave / 2);
+      return (blockIdx.x + (nfull + h / kParts) * nb) * kWave + (h % kParts) * (kWave / kParts);
     } else {
       return u * kWave;
     }
   };
-  const auto unit_cnt = [&](uint32_t u) -> uint32_t { return kPool && u >= nfull ? kWave / 2 : kWave; };
+  const auto unit_cnt = [&](uint32_t u) -> uint32_t { return kPool && u >= nfull ? kWave / kParts : kWave; };
   bool pool_live = kPool;   // wave-uniform: no failed dequeue yet
   uint32_t tile, tn, tnn;   // pool units (kPool) or tiles
   if constexpr (kPool) {
@@ -1993,10 +1995,14 @@ struct Variant {
 #define XSKNF_SP(L, N, U) {L, N, U, 2, &launch_split<8, L, N, U, true, false, true>, XSKNF_GPU_KERNEL_SPLIT, 24}
 // one 12-wave block per CU, its waves drawing the CU's tiles from a shared pool (window field + 32)
 #define XSKNF_SC(L, N, U) {L, N, U, 0, &launch_split<8, L, N, U, true, false, false, 12>, XSKNF_GPU_KERNEL_SPLIT, 56}
+// jumbo: one 8-wave block per CU (176 VGPRs: 2 waves per SIMD), W = 4
+#define XSKNF_SC4(L, N, U) {L, N, U, 0, &launch_split<4, L, N, U, true, false, false, 8>, XSKNF_GPU_KERNEL_SPLIT, 52}
+// (A/B) jumbo with one 12-wave block per CU (window field + 64)
+#define XSKNF_SC4W(L, N, U) {L, N, U, 0, &launch_split<4, L, N, U, true, false, false, 12>, XSKNF_GPU_KERNEL_SPLIT, 116}
 const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
     XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_SC(16, 2, 2), XSKNF_S(8, 16, 3, 1, 1),
-    XSKNF_S(4, 16, 3, 2, 1),
+    XSKNF_S(4, 16, 3, 2, 1), XSKNF_SC4(16, 3, 2),
     // ... the lane kernel for short frames ...
     XSKNF_L(5, 2),
     // ... and the zero-copy host path's small-batch group shapes (host_path.hip)
@@ -2009,6 +2015,7 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
+    XSKNF_SC4W(16, 3, 2),
     XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
     XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
     XSKNF_SP(16, 2, 2), XSKNF_SP(16, 3, 1),         // window prefetch: +3-6 us on 1500 / IMIX / 570 (tune_pfw)
@@ -2029,6 +2036,8 @@ const Variant kVariants[] = {
 #undef XSKNF_SD
 #undef XSKNF_SP
 #undef XSKNF_SC
+#undef XSKNF_SC4
+#undef XSKNF_SC4W
 
 const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   for (const Variant &v : kVariants) {
