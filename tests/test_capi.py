@@ -116,6 +116,6 @@ def test_launch_shape_for_lengths_without_gpu():
                                      plain.window_chunks, plain.fused_stores)
     assert shape(1500, 1500)[2] == 2 and shape(1500, 1500)[3] == 56
     assert shape(1500, 352)[3] == 24 and shape(1500, 511)[3] == 24 and shape(4000, 1024)[3] == 56
-    assert shape(9000, 9000)[3] == 20          # jumbo: 4-chunk window, whatever the mean
+    assert shape(9000, 9000)[3] == 52          # jumbo: 4-chunk window, tile pool, whatever the mean
     assert shape(64, 64)[1] == 1               # lane kernel
     assert lib.xsknf_gpu_launch_cfg_for_lens(1500, 1500, None) == -errno.EINVAL

@@ -2086,7 +2086,9 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   //    1024 B 201.5 vs 206.8, 570 B 148.7 vs 150.1, IMIX 115.8 vs 114.8
   //    (profiles/r02/ab_pool.jsonl);
   //  * jumbo: 4-chunk window, 16 x 3 items, two per group in flight, the
-  //    per-tile policy + scatter pass: 9000 B 1467 us [tail patches 1491].
+  //    per-tile policy + scatter pass: 9000 B 1467 us [tail patches 1491];
+  //    one 8-wave block per CU with the tile pool (+ 32): 1456 vs 1466 [12-wave
+  //    blocks 1520; tail patches 1598] (profiles/r02/ab_pool_jumbo.jsonl).
   c.kernel = XSKNF_GPU_KERNEL_SPLIT;
   c.lanes_per_frame = 16;
   if (hint <= 128) {
@@ -2098,7 +2100,7 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
     c.window_chunks = 8 + 16 + (mean != 0 && mean < kPoolMinMean ? 0 : 32);
     c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   } else {
-    c.window_chunks = 4 + 16; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
+    c.window_chunks = 4 + 16 + 32; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
   }
 }
 
