@@ -1270,29 +1270,31 @@ void checksum_kernel_split(const KernelArgs args) {
   int it = 0;              // tiles done by this wave
   bool any_entry = false;  // wave-uniform: the patch list holds an entry
   // The wave's tiles: `tile`, then `tn`, `tnn` (kNoTile: none).
-  // * SW = 4 (several blocks per CU): every waves-th tile from the wave's index.
-  // * kPool (SW = 12: one block holds every wave of its CU): the block's tiles,
-  //   every nb-th from the block index, are a pool its waves draw from -- the
-  //   first three rounds by wave index, then through an LDS counter, three tiles
-  //   ahead.  A CU's waves do not stream equally fast: with three 4-wave blocks
-  //   per CU the third block's waves ended their streams ~40 us after the first
-  //   two's at 1500 B, and the launch waits for the last one
-  //   (tools/timeline.py); from a shared pool the faster waves take more tiles.
-  //   A tile past the wave's patch list writes its checks in-line.  (A global
-  //   counter was tried: its atomics retire in vmcnt order, and each round trip
+  // * SW = 4 (several blocks per CU): every waves-th tile from the wave's index,
+  //   descriptors two tiles ahead.
+  // * kPool (one block holds every wave of its CU: SW = 12, or 8 for jumbo):
+  //   the block's tiles, every nb-th from the block index, are a pool of units
+  //   its waves draw from -- the first by wave index, each later one claimed
+  //   through an LDS counter when the wave starts a unit, its descriptors
+  //   loaded while that unit streams.  A CU's waves do not stream equally fast
+  //   (three 4-wave blocks per CU: the third block's waves ended their streams
+  //   ~40 us after the first two's at 1500 B, tools/timeline.py), and from a
+  //   shared pool the faster ones take more units.  A unit past the wave's
+  //   patch list writes its checks in-line.  (Per-XCD global counters were
+  //   tried: a device-scope atomic retires in vmcnt order, and each round trip
   //   held up the next load wait -- 1500 B 347 vs 291 us.)
   const uint32_t ntiles = (args.n + kWave - 1) / kWave;
   __shared__ uint32_t pool_next;
   const uint32_t nb = gridDim.x;
   const uint32_t bt = ntiles > blockIdx.x ? (ntiles - blockIdx.x + nb - 1) / nb : 0u;   // the block's tiles
   // The pool's units: the block's tiles, except that its last SW tiles run as
-  // two 32-frame halves each, so the waves' streams end within half a tile of
-  // each other (whole tiles: 46 us apart at 1500 B, one tile's time).
+  // kParts parts each, so the waves' streams end closer together: halves up to
+  // 4 KiB (quarters there: 570 B 165 vs 151 us, 1024 B 213 vs 205 --
+  // profiles/r02/ab_pool.jsonl), quarters for jumbo tiles (W = 4), which
+  // stream for ~160 us each.  XSKNF_POOL_HALVES=0 (A/B): whole tiles only.
 #ifndef XSKNF_POOL_HALVES
 #define XSKNF_POOL_HALVES 1
 #endif
-  // (16-frame quarters for the last SW tiles, A/B: 570 B 165 vs 151 us, 1024 B 213 vs 205 -- ab_pool.jsonl)
-  // jumbo tiles (W = 4) end in quarters: a 64-frame tile of 9000 B frames streams for ~160 us
   constexpr uint32_t kParts = W == 4 ? 4u : 2u;
   const uint32_t nsplit = kPool && XSKNF_POOL_HALVES ? min(bt, static_cast<uint32_t>(SW)) : 0u;
   const uint32_t nfull = bt - nsplit;
@@ -1312,11 +1314,10 @@ void checksum_kernel_split(const KernelArgs args) {
   bool pool_live = kPool;   // wave-uniform: no failed dequeue yet
   uint32_t tile, tn, tnn;   // pool units (kPool) or tiles
   if constexpr (kPool) {
-    // one unit ahead only: a wave holds at most the unit it sums and the next
-    // (three ahead, the waves of a block ended 43 us apart at 1500 B: 284.5 vs
-    // 279.2 us; claiming when the unit's payload starts instead of at its
-    // start: 1500 B a tie, 570 B 149.1 vs 146.7, IMIX 118.5 vs 115.9 --
-    // profiles/r02/ab_pool.jsonl)
+    // a wave holds at most the unit it sums and the next (claimed three ahead,
+    // the waves of a block ended 43 us apart at 1500 B: 284.5 vs 279.2 us;
+    // claimed when the unit's payload starts rather than at its start: 1500 B a
+    // tie, 570 B 149.1 vs 146.7, IMIX 118.5 vs 115.9 -- profiles/r02/ab_pool.jsonl)
     tile = pool_unit(wv);
     tn = tnn = kNoTile;
     if (threadIdx.x == 0) pool_next = SW;
