@@ -507,3 +507,33 @@ def test_patch_list_overflow_takes_the_record_path(dev, shape):
     _, ov = O.c_time_batch(host, hd, threads=16, reps=1)
     assert np.array_equal(v.cpu().numpy(), ov)
     assert np.array_equal(umem.cpu().numpy(), host)
+
+
+@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 0, 1, 52)], ids=["pool-w8", "pool-jumbo"])
+@pytest.mark.parametrize("n", [1, 17, 33, 95, 12 * 64 + 5, 3 * 12 * 64 - 7, 256 * 12 * 64 + 4095])
+def test_pool_units_cover_every_frame(dev, shape, n):
+    """The CU-wide tile pool (window + 32): the block's last tiles run as
+    halves (W = 8) or quarters (jumbo), and a batch whose length is not a
+    multiple of 64, 32 or 16 leaves partial and empty units; batches from one
+    frame to more than a full grid of tiles, every frame bit-exact."""
+    import ctypes
+    from xsknf_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(n)
+    lens = rng.integers(40, 1600 if shape[6] == 56 else 9000, size=n).astype(np.uint32)
+    if shape[6] == 56:
+        b = frames.aligned_batch(n, np.minimum(lens, 1792), chunk=2048, seed=n)
+    else:
+        b = frames.unaligned_batch(n, lens, seed=n)
+    frames.inject_edge_cases(b, 0.05)
+    ou, ov = run_oracle(b)
+    umem = torch.from_numpy(b.umem).to(dev)
+    descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+    v = torch.empty(b.n, dtype=torch.int32, device=dev)
+    assert lib.xsknf_gpu_checksum_batch_cfg(
+        ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), b.n, 0,
+        ctypes.byref(_lib.CsumOpts(1, O.REDIRECT, 1, 0)), ctypes.c_void_p(v.data_ptr()),
+        ctypes.byref(launch_cfg(shape, bpc=8)), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), ov)
+    assert np.array_equal(umem.cpu().numpy(), ou)
