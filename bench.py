@@ -270,6 +270,8 @@ def time_workload(name, args, world, rank, dev, seed, primary):
               "checks deferred to a scatter_checks launch")
     family = ("checksum_kernel_split" if cfg.kernel == 1 else
               "checksum_kernel_lane" if cfg.lanes_per_frame == 1 else "checksum_kernel")
+    if cfg.kernel == 1 and cfg.window_chunks & 32:
+        family += ", one block per CU, tile pool"
     k_ms = None
     if primary and args.kernel_steps > 0 and (cfg.fused_stores & 3) != 1:
         cfg.fused_stores = 3
@@ -303,6 +305,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     counters = allreduce_sum_i64([n, bytes_len, int((vh == -1).sum()), int((vh >= 0).sum())], world)
     shape = {"lanes_per_frame": cfg.lanes_per_frame, "chunks_per_lane": cfg.chunks_per_lane,
              "items_in_flight": cfg.frames_per_group, "window_chunks": cfg.window_chunks & 15,
+             "tile_pool": bool(cfg.kernel == 1 and cfg.window_chunks & 32),
              "frame_len_max": hint, "frame_len_mean": mean}
     return dict(name=name, desc=desc, n=n, K=K, lens=lens, bytes_len=bytes_len, step_ms=step_ms, stores=stores,
                 shape=shape,
