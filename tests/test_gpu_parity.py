@@ -271,6 +271,8 @@ AB_SHAPES = [
     # 16 x 3 items with the 8-tile patch list (long-frame batches, not in the product)
     (16, 3, 2, 0, 18, 1, 24), (16, 3, 2, 0, 2, 1, 24), (16, 3, 2, 0, 0, 1, 24), (16, 3, 2, 0, 1, 1, 24),
     (16, 3, 2, 0, 0, 1, 116), (16, 3, 2, 0, 18, 1, 116),
+    # the lane kernel with one 16-wave block per CU sharing the CU's tiles (window field 32)
+    (1, 5, 2, 0, 1, 0, 32), (1, 5, 2, 0, 9, 0, 32), (1, 5, 2, 0, 2, 0, 32), (1, 5, 2, 0, 0, 0, 32),
     # split kernel with LDS-DMA phase B (ring 1) / window prefetch (ring 2): every check deferred only
     (16, 2, 2, 1, 18, 1, 24), (16, 4, 1, 1, 2, 1, 24), (16, 2, 2, 2, 18, 1, 24), (16, 3, 1, 2, 2, 1, 24),
 ]
@@ -509,7 +511,10 @@ def test_patch_list_overflow_takes_the_record_path(dev, shape):
     assert np.array_equal(umem.cpu().numpy(), host)
 
 
-@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 0, 1, 52)], ids=["pool-w8", "pool-jumbo"])
+@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 0, 1, 52),
+                                   pytest.param((1, 5, 2, 0, 1, 0, 32),
+                                                marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only"))],
+                         ids=["pool-w8", "pool-jumbo", "pool-lane"])
 @pytest.mark.parametrize("n", [1, 17, 33, 95, 12 * 64 + 5, 3 * 12 * 64 - 7, 256 * 12 * 64 + 4095])
 def test_pool_units_cover_every_frame(dev, shape, n):
     """The CU-wide tile pool (window + 32): the block's last tiles run as
@@ -520,8 +525,8 @@ def test_pool_units_cover_every_frame(dev, shape, n):
     from xsknf_amd import _lib
     lib = _lib.load()
     rng = np.random.default_rng(n)
-    lens = rng.integers(40, 1600 if shape[6] == 56 else 9000, size=n).astype(np.uint32)
-    if shape[6] == 56:
+    lens = rng.integers(40, {56: 1600, 52: 9000, 32: 129}[shape[6]], size=n).astype(np.uint32)
+    if shape[6] != 52:
         b = frames.aligned_batch(n, np.minimum(lens, 1792), chunk=2048, seed=n)
     else:
         b = frames.unaligned_batch(n, lens, seed=n)

@@ -743,29 +743,57 @@ __device__ __forceinline__ FrameRef lane_ref(const KernelArgs &a, const uint4 d,
   return make_ref(a, (static_cast<uint64_t>(d.y) << 32) | d.x, d.z, f < a.n);
 }
 
-template <int NCH, int SPT>
-__global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs args) {
+constexpr uint32_t kNoTile = 0xffffffffu;   // no tile / unit
+
+// SW > 4 (one 16-wave block per CU): the block's tiles, every nb-th from the
+// block index, are a pool its waves claim from through an LDS counter, one
+// tile ahead, as the split kernel's pool (a CU's waves do not stream equally
+// fast; from a shared pool the faster ones take more tiles).
+template <int NCH, int SPT, int SW = kWavesPerBlock>
+__global__ __launch_bounds__(SW * kWave) void checksum_kernel_lane(const KernelArgs args) {
   constexpr uint32_t T = SPT * kWave;        // frames per tile
-  __shared__ __attribute__((aligned(16))) uint8_t hdr[kWavesPerBlock][kWave][kLaneSlot];
+  constexpr bool kPool = SW > kWavesPerBlock;
+  __shared__ __attribute__((aligned(16))) uint8_t hdr[SW][kWave][kLaneSlot];
+  __shared__ uint32_t pool_next;
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t slot = lds_addr(&hdr[wv][lane][0]);
-  const uint32_t waves = gridDim.x * kWavesPerBlock;
+  const uint32_t waves = gridDim.x * SW;
   const uint32_t last = args.n - 1;
+  const uint32_t ntiles = (args.n + T - 1) / T, nb = gridDim.x;
+  const uint32_t bt = ntiles > blockIdx.x ? (ntiles - blockIdx.x + nb - 1) / nb : 0u;   // the block's tiles
 
-  uint32_t tile = blockIdx.x * kWavesPerBlock + wv;
+  uint32_t tile;
+  if constexpr (kPool) {
+    tile = static_cast<uint32_t>(wv) < bt ? blockIdx.x + wv * nb : kNoTile;
+    if (threadIdx.x == 0) pool_next = SW;
+    __syncthreads();
+  } else {
+    tile = blockIdx.x * SW + wv < ntiles ? blockIdx.x * SW + wv : kNoTile;
+  }
+  const auto desc_at = [&](uint32_t t, int st) {
+    return *reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(t * T + st * kWave + lane, last)));
+  };
   uint32_t nrec = 0;
   uint4 dn[SPT];
 #pragma unroll
-  for (int st = 0; st < SPT; ++st)
-    dn[st] = *reinterpret_cast<const uint4 *>(args.descs + min(tile * T + st * kWave + lane, last));
-  for (; tile * T < args.n; tile += waves) {
+  for (int st = 0; st < SPT; ++st) dn[st] = desc_at(tile, st);
+  while (tile != kNoTile) {
     const uint32_t tf0 = tile * T;
+    uint32_t next;
+    if constexpr (kPool) {
+      uint32_t dq = 0;
+      if (lane == 0) dq = __hip_atomic_fetch_add(&pool_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint32_t p = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dq), 0));
+      next = p < bt ? blockIdx.x + p * nb : kNoTile;
+    } else {
+      next = tile + waves < ntiles ? tile + waves : kNoTile;
+    }
     uint4 d[SPT];
 #pragma unroll
     for (int st = 0; st < SPT; ++st) {
       d[st] = dn[st];
-      dn[st] = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * T + st * kWave + lane, last));
+      dn[st] = desc_at(next, st);
     }
     uint4 v[2][NCH];
     FrameRef r[2];
@@ -784,6 +812,7 @@ __global__ __launch_bounds__(kBlock) void checksum_kernel_lane(const KernelArgs 
       nrec += store_result(args, f, f < args.n, o.res);
       compiler_barrier();   // the next frame rewrites this lane's header window
     }
+    tile = next;
   }
   publish_records(args, nrec, lane);
 }
@@ -1215,8 +1244,6 @@ __device__ __forceinline__ void timeline_put(uint32_t wave, int lane, unsigned l
   if (p && lane < 8) p[8ull * wave + lane] = x;
 }
 #endif
-
-constexpr uint32_t kNoTile = 0xffffffffu;
 
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
@@ -1951,10 +1978,10 @@ int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel launch");
 }
 
-template <int NCH, int SPT>
+template <int NCH, int SPT, int SW = kWavesPerBlock>
 int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  auto k = checksum_kernel_lane<NCH, SPT>;
-  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, SPT * kWave)), dim3(kBlock), 0, stream, a);
+  auto k = checksum_kernel_lane<NCH, SPT, SW>;
+  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, SPT * kWave, SW)), dim3(SW * kWave), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
 
@@ -1987,6 +2014,8 @@ struct Variant {
 
 #define XSKNF_V(L, N, S) {L, N, S, 0, &launch_reg<L, N, S>}
 #define XSKNF_L(N, S) {1, N, S, 0, &launch_lane<N, S>}
+// lane kernel, one 16-wave block per CU with the tile pool (window field 32)
+#define XSKNF_LP(N, S) {1, N, S, 0, &launch_lane<N, S, 16>, XSKNF_GPU_KERNEL_AUTO, 32}
 #define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
 // split: window field = W, + 16 for the transposed (coalesced) window load
 #define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL, false>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
@@ -2017,6 +2046,7 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
     XSKNF_SC4W(16, 3, 2),
+    XSKNF_LP(5, 2),   // lane kernel with the tile pool: 64 B 59.65 vs 59.51 us, a tie (r02 ab_pool_lane.jsonl)
     XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
     XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
     XSKNF_SP(16, 2, 2), XSKNF_SP(16, 3, 1),         // window prefetch: +3-6 us on 1500 / IMIX / 570 (tune_pfw)
@@ -2032,6 +2062,7 @@ const Variant kVariants[] = {
 };
 #undef XSKNF_V
 #undef XSKNF_L
+#undef XSKNF_LP
 #undef XSKNF_D
 #undef XSKNF_S
 #undef XSKNF_SD
@@ -2048,7 +2079,7 @@ const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
           v.window == c.window_chunks && v.ring == c.lds_ring)
         return &v;
     } else if (v.lpf == c.lanes_per_frame && v.nch == c.chunks_per_lane && v.ring == c.lds_ring &&
-               (c.lds_ring || v.u == c.frames_per_group)) {
+               (c.lds_ring || v.u == c.frames_per_group) && v.window == (c.window_chunks & 32)) {
       return &v;
     }
   }
