@@ -1,7 +1,7 @@
 set -o pipefail
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/lp_tests.log 2>&1; rc=$?; tail -3 gpurun_out/lp_tests.log
-[ $rc = 0 ] || { grep -E "FAILED|Error" gpurun_out/lp_tests.log | head; exit 1; }
 for r in 1 2 3; do
-timeout -k 10 200 python tools/tune.py --workload 64 --rotate 13 --bpc 8 --rounds 5 --variants 1,5,2,0,1,0,32 >> gpurun_out/lp_tune.jsonl 2>>gpurun_out/lp_tune.err || { tail gpurun_out/lp_tune.err; exit 1; }
+  for L in xsknf_amd/lib build/nohalf; do
+    XSKNF_GPU_LIB=$PWD/$L/libxsknf_gpu.so timeout -k 10 200 python tools/tune.py --workload imix --rotate 4 --bpc 4 --rounds 4 --variants 16,2,2,0,18,1,56 2>>gpurun_out/imix_nh.err | sed "s|^{|{\"lib\": \"$L\", |" >> gpurun_out/imix_nh.jsonl || exit 1
+  done
 done
-cut -c1-200 gpurun_out/lp_tune.jsonl
+cut -c1-200 gpurun_out/imix_nh.jsonl
