@@ -1981,6 +1981,15 @@ int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
 template <int NCH, int SPT, int SW = kWavesPerBlock>
 int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   auto k = checksum_kernel_lane<NCH, SPT, SW>;
+  if constexpr (SW > kWavesPerBlock) {   // as launch_split: a CU-sized block the device cannot hold
+    static thread_local int fits = -1;
+    if (fits < 0) {
+      int b = 0;
+      fits = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, SW * kWave, 0) == hipSuccess && b > 0;
+      (void)hipGetLastError();
+    }
+    if (!fits) return launch_lane<NCH, SPT, kWavesPerBlock>(a, stream, blocks_per_cu);
+  }
   hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, SPT * kWave, SW)), dim3(SW * kWave), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
@@ -1990,6 +1999,17 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   // the DMA stages / the window prefetch reuse the windows: every check deferred
   if ((DMA || PFW) && a.defer_min_len != 0) return -EINVAL;
   auto k = checksum_kernel_split<W, LPF, NCH, U, TL, DMA, PFW, SW>;
+  if constexpr (SW > kWavesPerBlock) {
+    // a block holding a whole CU's waves (and ~160 KiB of LDS) that the device
+    // cannot make resident runs as the 4-wave shape with the static schedule
+    static thread_local int fits = -1;
+    if (fits < 0) {
+      int b = 0;
+      fits = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, SW * kWave, 0) == hipSuccess && b > 0;
+      (void)hipGetLastError();
+    }
+    if (!fits) return launch_split<W, LPF, NCH, U, TL, DMA, PFW, kWavesPerBlock>(a, stream, blocks_per_cu);
+  }
   hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave, SW)), dim3(SW * kWave), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_split launch");
 }
