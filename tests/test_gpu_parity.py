@@ -484,11 +484,11 @@ def test_concurrent_streams(dev):
                                    pytest.param((16, 3, 2, 0, 18, 1, 24),
                                                 marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only"))],
                          ids=_shape_id)
-def test_patch_list_overflow_takes_the_record_path(dev, shape):
+def test_patch_list_overflow_writes_in_line(dev, shape):
     """One block per CU: every wave gets more tiles than its LDS patch list
-    holds (6, or 8 for the A/B 16 x 3 shape), so its later tiles park records in `verdicts` and are
-    patched by the record path (tail_scatter) after the list; every verdict and
-    byte still matches the oracle."""
+    holds (6, 7 with the pool, 8 for the A/B 16 x 3 shape), so its later tiles
+    write their checks in-line; every verdict and byte still matches the
+    oracle."""
     import ctypes
     from xsknf_amd import _lib
     lib = _lib.load()

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of tail-patch batching (XSKNF_TAIL_TILES builds) on the 1500 B and IMIX steps (run ON the GPU box).
+# A/B of tail-patch batching (XSKNF_PATCH_T builds; the XSKNF_TAIL_TILES record path is gone) on the 1500 B and IMIX steps (run ON the GPU box).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for R in 1 2; do

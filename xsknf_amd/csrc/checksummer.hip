@@ -467,7 +467,7 @@ __device__ unsigned long long g_rec_count[kCountSlots][kCountLanes][kCountStride
 // atomic per tile would hold every following vmcnt wait on its L2 round trip.
 __device__ __forceinline__ uint32_t store_result(const KernelArgs &a, uint32_t f, bool valid, int32_t v) {
   if (valid) a.verdicts[f] = v;
-  if (!a.count_records && !a.tail_scatter) return 0;
+  if (!a.count_records) return 0;
   return static_cast<uint32_t>(__builtin_popcountll(
       __builtin_amdgcn_ballot_w64(valid && (static_cast<uint32_t>(v) & kRecTagMask) == kRecTag)));
 }
@@ -1036,92 +1036,6 @@ struct ItemStageDMA {
   }
 };
 
-// The deferred checks of a wave's own tiles, patched by the wave itself after
-// its last tile (KernelArgs::tail_scatter): the write-only pass of
-// scatter_checks without a second launch, and without waiting for the slowest
-// wave of the grid.  The wave's record stores are complete (vmcnt 0) before it
-// reads them back (non-temporal loads: from L2, where they landed).  A tile
-// with no record costs one 256-byte read.  Per round 16 frames, 4 lanes each,
-// as the dense scatter shape: the lanes of a frame rewrite its check's 64-byte
-// sector with one non-temporal store (2 bytes where the sector leaves the frame).
-#ifndef XSKNF_TAIL_TILES
-#define XSKNF_TAIL_TILES 2
-#endif
-constexpr int kTailTiles = XSKNF_TAIL_TILES;   // tiles whose patches are in flight together
-
-__device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t tile0, uint32_t waves, int lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int piece = lane & 3;
-  constexpr int T = kTailTiles;
-  for (uint32_t tb = tile0; tb * kWave < args.n; tb += T * waves) {
-    // the records of T tiles, then their descriptors, then their sectors: three
-    // round trips for T tiles instead of two per tile
-    uint32_t r[T];
-    bool rec[T];
-    uint64_t any = 0;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const uint32_t f = (tb + t * waves) * kWave + lane;
-      r[t] = f < args.n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(args.verdicts) + f) : 0u;
-    }
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      rec[t] = (r[t] & kRecTagMask) == kRecTag;
-      any |= __builtin_amdgcn_ballot_w64(rec[t]);
-    }
-    if (!any) continue;
-    uint32_t rr[T][4];
-    xsknf_gpu_desc d[T][4];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const uint32_t tile = tb + t * waves;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int src = 16 * k + (lane >> 2);
-        rr[t][k] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(r[t])));
-        d[t][k] = args.descs[min(tile * kWave + src, args.n - 1)];
-      }
-    }
-    uint4 v[T][4];
-    uint8_t *mine[T][4];
-    int o[T][4];
-    bool whole[T][4], has[T][4];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        has[t][k] = (rr[t][k] & kRecTagMask) == kRecTag;   // src < n: records exist only there
-        uint8_t *fp = args.umem + umem_offset(d[t][k].addr);
-        uint8_t *chk = fp + ((rr[t][k] >> 16) & 0x7f) + 6;
-        uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);   // keeps global addressing
-        whole[t][k] = has[t][k] && sec >= fp && sec + 64 <= fp + d[t][k].len &&
-                      (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
-        mine[t][k] = whole[t][k] ? sec + 16 * piece : chk;
-        o[t][k] = static_cast<int>(chk - mine[t][k]);
-        if (whole[t][k]) v[t][k] = load_nt(reinterpret_cast<const uint4 *>(mine[t][k]));
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint16_t c = static_cast<uint16_t>(rr[t][k]);
-        if (whole[t][k]) {
-          uint4 w = put_byte(v[t][k], o[t][k], c);
-          w = put_byte(w, o[t][k] + 1, c >> 8);
-          store_nt16(mine[t][k], w);
-        } else if (has[t][k] && piece == 0) {
-          XSKNF_GST(mine[t][k], 2) {
-            mine[t][k][0] = static_cast<uint8_t>(c);
-            mine[t][k][1] = static_cast<uint8_t>(c >> 8);
-          }
-        }
-      }
-      if (rec[t]) args.verdicts[(tb + t * waves) * kWave + lane] = args.fwd_verdict;
-    }
-  }
-}
-
 // The patch list: where the default shape (W = 8, two items in flight: 157
 // VGPRs, 3 waves per SIMD, so 3 blocks per CU) has LDS to spare, a deferred
 // check is not parked in `verdicts` but kept in the wave's LDS list, one
@@ -1130,8 +1044,11 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
 // sector, byte of the check in the sector, the check}.  The frame's final
 // verdict is stored in the tile's one verdict store, and the wave's patches
 // read neither records nor descriptors back: one round trip (the sectors)
-// instead of three.  Tiles past kPatchTiles (a wave with more tiles than that:
-// grids smaller than residency) take the record path (tail_scatter).
+// instead of three.  A wave's tiles past its list (grids smaller than
+// residency, or a pool's faster waves) write their checks in-line.  (Parking
+// those as records in `verdicts` for the wave to patch after its list -- a
+// record path with three round trips -- raised an illegal-address fault twice
+// in full GPU suites, never alone or under the guard build: removed)
 #ifndef XSKNF_PATCH_TILES
 #define XSKNF_PATCH_TILES 6
 #endif
@@ -1435,8 +1352,8 @@ void checksum_kernel_split(const KernelArgs args) {
     const bool to_list = list_ok && it < PT;   // wave-uniform
     // per-tile store policy, as the register kernel: long frames defer their
     // checks only where they are at least half of the tile
-    // (a pooled wave's tiles past its list: in-line; the record path walks the static schedule)
-    uint32_t defer_min = kPool && args.tail_scatter && !to_list ? kNoDefer : args.defer_min_len;
+    // (a wave's tiles past its patch list: in-line)
+    uint32_t defer_min = args.tail_scatter && !to_list ? kNoDefer : args.defer_min_len;
     if (defer_min != kNoDefer && defer_min != 0 && !args.no_scatter) {
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(f < args.n && d.z >= defer_min)));
@@ -1613,8 +1530,6 @@ void checksum_kernel_split(const KernelArgs args) {
 #endif
   if (args.tail_scatter) {
     if (any_entry) tail_patch_list(args, pl, min(it, PT), lane, it <= PT, area, kSlot);
-    if (__builtin_amdgcn_readfirstlane(nrec))
-      tail_scatter(args, blockIdx.x * SW + wv + (list_ok ? PT : 0) * waves, waves, lane);   // static schedule only
   } else {
     publish_records(args, nrec, lane);
   }
@@ -2200,6 +2115,9 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   // + 16: the split kernel patches its deferred checks itself (no scatter launch)
   a.tail_scatter = (cfg.fused_stores & 16) && v->kernel == XSKNF_GPU_KERNEL_SPLIT && a.defer_min_len != kNoDefer &&
                    !a.no_scatter;
+  // the patch list indexes 64-byte sectors in 32 bits: a larger UMEM parks its
+  // checks for the scatter pass instead
+  if (a.umem_size >= kPatchMaxUmem) a.tail_scatter = 0;
   a.count_records = a.defer_min_len != kNoDefer && !a.no_scatter && !a.tail_scatter;
   // A batch larger than kLaunchFrames runs as consecutive launches of that many
   // frames: one launch over the whole of an 8M-frame IMIX batch (config 4 on
