@@ -1185,7 +1185,7 @@ void checksum_kernel_split(const KernelArgs args) {
   // patch list tiles: 16 x 2 items fit 3 waves per SIMD (6 tiles per wave at 1M
   // frames), 16 x 3 fit 2 (8 tiles per wave)
   constexpr bool kPool = SW > kWavesPerBlock;   // one block per CU: its waves share the CU's tiles
-  constexpr int PT = (W == 8 && U == 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
+  constexpr int PT = (W == 8 && U >= 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
   __shared__ __attribute__((aligned(16))) uint2 plist[SW][PT > 0 ? PT * kWave : 1];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -1980,7 +1980,7 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
-    XSKNF_SC4W(16, 3, 2),
+    XSKNF_SC4W(16, 3, 2), XSKNF_SC(16, 2, 3),
     XSKNF_LP(5, 2),   // lane kernel with the tile pool: 64 B 59.65 vs 59.51 us, a tie (r02 ab_pool_lane.jsonl)
     XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
     XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
