@@ -1185,6 +1185,8 @@ void checksum_kernel_split(const KernelArgs args) {
   // patch list tiles: 16 x 2 items fit 3 waves per SIMD (6 tiles per wave at 1M
   // frames), 16 x 3 fit 2 (8 tiles per wave)
   constexpr bool kPool = SW > kWavesPerBlock;   // one block per CU: its waves share the CU's tiles
+  // (jumbo keeps no list: with the pool and a 16-unit list, patching after the last unit tied the
+  // scatter pass, 1463 vs 1461 us -- profiles/r02/ab_jumbo_tail.jsonl)
   constexpr int PT = (W == 8 && U >= 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
   __shared__ __attribute__((aligned(16))) uint2 plist[SW][PT > 0 ? PT * kWave : 1];
 
