@@ -16,10 +16,12 @@ itself (one process per GPU, RCCL); the parent never touches the GPU.  On a box
 with fewer than N GPUs the ranks share the devices over gloo (a rehearsal of
 the N-rank path, marked `rehearsal` in the line).  Rank 0 prints ONE JSON line.
 
-Secondary workloads (timed after the primary, reported under `secondary`):
-64 B (config 2) and config 4 -- the global 8,388,608-frame IMIX batch split
-into byte-balanced contiguous shards, one per rank (all of it on one GPU at
-N = 1, exactly config 4's 8-way split at N = 8).
+Secondary workloads (timed after the primary, reported under `secondary`, each
+with its step fraction, kernel and committed PMC traffic): 64 B (config 2), a
+1M-frame IMIX batch (config 4's per-GPU shard), 9000 B jumbo frames in an
+unaligned UMEM (config 5), and config 4 -- the global 8,388,608-frame IMIX batch
+split into byte-balanced contiguous shards, one per rank (all of it on one GPU
+at N = 1, exactly config 4's 8-way split at N = 8).
 """
 from __future__ import annotations
 
@@ -67,7 +69,7 @@ def parse():
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU (config4: global frames "
                    f"= {CONFIG4_FRAMES} unless --config4-frames)")
     p.add_argument("--config4-frames", type=int, default=CONFIG4_FRAMES)
-    p.add_argument("--secondary", default="64,config4",
+    p.add_argument("--secondary", default="64,imix,jumbo,config4",
                    help="comma list of extra workloads timed after the primary ('' = none)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
@@ -480,6 +482,9 @@ def step_summary(r, steps):
            "wall_ms_per_step": round(r["wall_max"] / steps * 1e3, 4), "rotated_batches": r["K"]}
     if r["span"] is not None:
         out["rank0_shard"] = list(r["span"])
+    out["kernel"] = f"{r['family']} ({r['stores']})"
+    out["launch_shape"] = r["shape"]
+    out["traffic"] = traffic_for(r["name"])
     return out
 
 

@@ -466,8 +466,14 @@ __device__ unsigned long long g_rec_count[kCountSlots][kCountLanes][kCountStride
 // (wave-uniform), which the wave adds up and publishes once, at exit: an
 // atomic per tile would hold every following vmcnt wait on its L2 round trip.
 __device__ __forceinline__ uint32_t store_result(const KernelArgs &a, uint32_t f, bool valid, int32_t v) {
-  if (valid) a.verdicts[f] = v;
+  if (valid) {
+    XSKNF_GST(a.verdicts + f, 4) a.verdicts[f] = v;
+  }
+#ifdef XSKNF_RECORD_PATH
+  if (!a.count_records && !a.tail_scatter) return 0;
+#else
   if (!a.count_records) return 0;
+#endif
   return static_cast<uint32_t>(__builtin_popcountll(
       __builtin_amdgcn_ballot_w64(valid && (static_cast<uint32_t>(v) & kRecTagMask) == kRecTag)));
 }
@@ -650,7 +656,7 @@ constexpr int kLaneSlot = 16 * kHdrChunks;   // per-lane LDS header window
 template <int NCH>
 __device__ __forceinline__ void load_lane(const FrameRef &r, uint4 (&v)[NCH]) {
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) v[k] = r.cp[min(k, r.nch - 1)];
+  for (int k = 0; k < NCH; ++k) v[k] = *XSKNF_GLD(r.cp + min(k, r.nch - 1), 16);
 }
 
 // A lane's result; when `sector` is set, the frame's patched 64-byte check
@@ -671,7 +677,7 @@ __device__ __forceinline__ LaneOut process_lane(const KernelArgs &args, const Fr
 #pragma unroll
   for (int k = 0; k < NCH; ++k) lds_store_u128(slot + 16 * k, v[k]);
   const int need = min(kHdrChunks, r.nch);   // header bytes past the window (large ihl)
-  for (int k = NCH; k < need; ++k) lds_store_u128(slot + 16 * k, r.cp[k]);
+  for (int k = NCH; k < need; ++k) lds_store_u128(slot + 16 * k, *XSKNF_GLD(r.cp + k, 16));
   compiler_barrier();
   const Header h = parse_header(slot + r.rs);
   compiler_barrier();
@@ -686,7 +692,7 @@ __device__ __forceinline__ LaneOut process_lane(const KernelArgs &args, const Fr
   uint32_t acc_lo = 0, acc_hi = 0;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) chunk_sum(v[k], 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
-  for (int k = NCH; k < r.nch; ++k) chunk_sum(r.cp[k], 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
+  for (int k = NCH; k < r.nch; ++k) chunk_sum(*XSKNF_GLD(r.cp + k, 16), 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
   const uint16_t c = check_of(h, acc_lo + (acc_hi << 8), args.payload_mult);
   if (static_cast<uint32_t>(r.len) >= args.defer_min_len) {
     out.res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
@@ -707,7 +713,7 @@ __device__ __forceinline__ LaneOut process_lane(const KernelArgs &args, const Fr
     out.lds_sec = slot + static_cast<uint32_t>(sec - c0);
     out.gsec = r.fp + static_cast<intptr_t>(sec - f0);   // global addressing from fp
   } else {
-    *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+    XSKNF_GST(r.fp + h.u + 6, 2) *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
   }
   return out;
 }
@@ -732,8 +738,11 @@ __device__ __forceinline__ void store_sectors(const LaneOut &o, int lane, bool p
     if ((any >> src) & 1) {
       uint8_t *g = reinterpret_cast<uint8_t *>((static_cast<uintptr_t>(hi) << 32) | lo);
       const uint4 w = lds_u128(ls + 16 * (lane & 3));
-      if (plain) *reinterpret_cast<uint4 *>(g + 16 * (lane & 3)) = w;
-      else store_nt16(g + 16 * (lane & 3), w);
+      if (plain) {
+        XSKNF_GST(g + 16 * (lane & 3), 16) *reinterpret_cast<uint4 *>(g + 16 * (lane & 3)) = w;
+      } else {
+        store_nt16(g + 16 * (lane & 3), w);
+      }
     }
   }
   compiler_barrier();
@@ -772,7 +781,7 @@ __global__ __launch_bounds__(SW * kWave) void checksum_kernel_lane(const KernelA
     tile = blockIdx.x * SW + wv < ntiles ? blockIdx.x * SW + wv : kNoTile;
   }
   const auto desc_at = [&](uint32_t t, int st) {
-    return *reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(t * T + st * kWave + lane, last)));
+    return *XSKNF_GLD(reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(t * T + st * kWave + lane, last))), 16);
   };
   uint32_t nrec = 0;
   uint4 dn[SPT];
@@ -1036,6 +1045,88 @@ struct ItemStageDMA {
   }
 };
 
+#ifdef XSKNF_RECORD_PATH
+// Debug only (`make guard-rec`, DESIGN 3 "The intermittent fault"): the record
+// path removed from the product in round 2, kept compilable so that the guard
+// build can run it.  A static-schedule wave's tiles past its patch list park
+// check records in `verdicts`; after its list the wave reads them back, then
+// their descriptors, then the sectors, and rewrites each sector whole.
+__device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t tile0, uint32_t waves, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int piece = lane & 3;
+  constexpr int T = 2;
+  for (uint32_t tb = tile0; tb * kWave < args.n; tb += T * waves) {
+    uint32_t r[T];
+    bool rec[T];
+    uint64_t any = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const uint32_t f = (tb + t * waves) * kWave + lane;
+      r[t] = f < args.n ? __builtin_nontemporal_load(XSKNF_GLD(reinterpret_cast<const uint32_t *>(args.verdicts) + f, 4))
+                        : 0u;
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      rec[t] = (r[t] & kRecTagMask) == kRecTag;
+      any |= __builtin_amdgcn_ballot_w64(rec[t]);
+    }
+    if (!any) continue;
+    uint32_t rr[T][4];
+    xsknf_gpu_desc d[T][4];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const uint32_t tile = tb + t * waves;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int src = 16 * k + (lane >> 2);
+        rr[t][k] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(r[t])));
+        d[t][k] = *XSKNF_GLD(args.descs + min(tile * kWave + src, args.n - 1), 16);
+      }
+    }
+    uint4 v[T][4];
+    uint8_t *mine[T][4];
+    int o[T][4];
+    bool whole[T][4], has[T][4];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        has[t][k] = (rr[t][k] & kRecTagMask) == kRecTag;
+        uint8_t *fp = args.umem + umem_offset(d[t][k].addr);
+        uint8_t *chk = fp + ((rr[t][k] >> 16) & 0x7f) + 6;
+        uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);
+        whole[t][k] = has[t][k] && sec >= fp && sec + 64 <= fp + d[t][k].len &&
+                      (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
+        mine[t][k] = whole[t][k] ? sec + 16 * piece : chk;
+        o[t][k] = static_cast<int>(chk - mine[t][k]);
+        if (whole[t][k]) v[t][k] = load_nt(reinterpret_cast<const uint4 *>(mine[t][k]));
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint16_t c = static_cast<uint16_t>(rr[t][k]);
+        if (whole[t][k]) {
+          uint4 w = put_byte(v[t][k], o[t][k], c);
+          w = put_byte(w, o[t][k] + 1, c >> 8);
+          store_nt16(mine[t][k], w);
+        } else if (has[t][k] && piece == 0) {
+          XSKNF_GST(mine[t][k], 2) {
+            mine[t][k][0] = static_cast<uint8_t>(c);
+            mine[t][k][1] = static_cast<uint8_t>(c >> 8);
+          }
+        }
+      }
+      if (rec[t]) {
+        int32_t *vp = args.verdicts + (tb + t * waves) * kWave + lane;
+        XSKNF_GST(vp, 4) *vp = args.fwd_verdict;
+      }
+    }
+  }
+}
+#endif
+
 // The patch list: where the default shape (W = 8, two items in flight: 157
 // VGPRs, 3 waves per SIMD, so 3 blocks per CU) has LDS to spare, a deferred
 // check is not parked in `verdicts` but kept in the wave's LDS list, one
@@ -1275,7 +1366,7 @@ void checksum_kernel_split(const KernelArgs args) {
     tnn = t0 + 2 * waves < ntiles ? t0 + 2 * waves : kNoTile;
   }
   const auto desc_of = [&](uint32_t t) {
-    return *reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(unit_f0(t) + lane, last)));
+    return *XSKNF_GLD(reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(unit_f0(t) + lane, last))), 16);
   };
   // descriptors travel two tiles ahead (static), one unit ahead (kPool)
   uint4 d = desc_of(tile);
@@ -1355,7 +1446,11 @@ void checksum_kernel_split(const KernelArgs args) {
     // per-tile store policy, as the register kernel: long frames defer their
     // checks only where they are at least half of the tile
     // (a wave's tiles past its patch list: in-line)
+#ifdef XSKNF_RECORD_PATH
+    uint32_t defer_min = kPool && args.tail_scatter && !to_list ? kNoDefer : args.defer_min_len;
+#else
     uint32_t defer_min = args.tail_scatter && !to_list ? kNoDefer : args.defer_min_len;
+#endif
     if (defer_min != kNoDefer && defer_min != 0 && !args.no_scatter) {
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(f < args.n && d.z >= defer_min)));
@@ -1373,7 +1468,7 @@ void checksum_kernel_split(const KernelArgs args) {
     {  // header bytes past the window (large ihl, or a frame start late in its chunk)
       const int u0 = 14 + 4 * static_cast<int>(lds_byte(slot + r.rs + 14) & 0x0f);
       const int need = min((r.rs + u0 + 8 + 15) >> 4, r.nch);
-      for (int k = W; k < need; ++k) lds_store_u128(slot + 16 * k, r.cp[k]);
+      for (int k = W; k < need; ++k) lds_store_u128(slot + 16 * k, *XSKNF_GLD(r.cp + k, 16));
     }
     compiler_barrier();
     const Header h = parse_header(slot + r.rs);
@@ -1532,6 +1627,10 @@ void checksum_kernel_split(const KernelArgs args) {
 #endif
   if (args.tail_scatter) {
     if (any_entry) tail_patch_list(args, pl, min(it, PT), lane, it <= PT, area, kSlot);
+#ifdef XSKNF_RECORD_PATH
+    if (!kPool && __builtin_amdgcn_readfirstlane(nrec))
+      tail_scatter(args, blockIdx.x * SW + wv + (list_ok ? PT : 0) * waves, waves, lane);
+#endif
   } else {
     publish_records(args, nrec, lane);
   }
@@ -1702,10 +1801,14 @@ __device__ __forceinline__ void rewrite_check(const KernelArgs &args, uint32_t f
     v = put_byte(v, o + 1, c >> 8);
     store_nt16(mine, v);
   } else if (piece == 0) {
-    chk[0] = static_cast<uint8_t>(c);
-    chk[1] = static_cast<uint8_t>(c >> 8);
+    XSKNF_GST(chk, 2) {
+      chk[0] = static_cast<uint8_t>(c);
+      chk[1] = static_cast<uint8_t>(c >> 8);
+    }
   }
-  if (piece == 0) args.verdicts[f] = args.fwd_verdict;
+  if (piece == 0) {
+    XSKNF_GST(args.verdicts + f, 4) args.verdicts[f] = args.fwd_verdict;
+  }
 }
 
 // Dense records (>= 1/4 of the frames): 4 lanes per frame over the whole grid;
@@ -1724,8 +1827,8 @@ __device__ __forceinline__ void scatter_dense(const KernelArgs &args) {
 #pragma unroll
     for (int k = 0; k < kScatterU; ++k) {
       const uint32_t f = min(t0 + k * nthreads, total - 1) >> 2;
-      r[k] = static_cast<uint32_t>(args.verdicts[f]);
-      d[k] = args.descs[f];
+      r[k] = static_cast<uint32_t>(*XSKNF_GLD(args.verdicts + f, 4));
+      d[k] = *XSKNF_GLD(args.descs + f, 16);
     }
     uint4 v[kScatterU];
     uint8_t *mine[kScatterU];
@@ -1752,10 +1855,14 @@ __device__ __forceinline__ void scatter_dense(const KernelArgs &args) {
         w = put_byte(w, o[k] + 1, c >> 8);
         store_nt16(mine[k], w);
       } else if (rec[k] && (t & 3) == 0) {
-        mine[k][0] = static_cast<uint8_t>(c);
-        mine[k][1] = static_cast<uint8_t>(c >> 8);
+        XSKNF_GST(mine[k], 2) {
+          mine[k][0] = static_cast<uint8_t>(c);
+          mine[k][1] = static_cast<uint8_t>(c >> 8);
+        }
       }
-      if (rec[k] && (t & 3) == 0) args.verdicts[t >> 2] = args.fwd_verdict;
+      if (rec[k] && (t & 3) == 0) {
+        XSKNF_GST(args.verdicts + (t >> 2), 4) args.verdicts[t >> 2] = args.fwd_verdict;
+      }
     }
   }
 }
@@ -1769,7 +1876,7 @@ __device__ __forceinline__ void scatter_sparse(const KernelArgs &args, uint8_t *
   const uint32_t waves = gridDim.x * kWavesPerBlock;
   for (uint32_t base = (blockIdx.x * kWavesPerBlock + wv) * kWave; base < args.n; base += waves * kWave) {
     const uint32_t f = base + lane;
-    const uint32_t r = f < args.n ? static_cast<uint32_t>(args.verdicts[f]) : 0u;
+    const uint32_t r = f < args.n ? static_cast<uint32_t>(*XSKNF_GLD(args.verdicts + f, 4)) : 0u;
     const bool rec = (r & kRecTagMask) == kRecTag;
     const uint64_t m = __builtin_amdgcn_ballot_w64(rec);
     if (!m) continue;
@@ -1784,7 +1891,7 @@ __device__ __forceinline__ void scatter_sparse(const KernelArgs &args, uint8_t *
       const int k = k0 + (lane >> 2);
       const int src = which[min(k, nrec - 1)];
       const uint32_t rs = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(r)));
-      if (k < nrec) rewrite_check(args, base + src, rs, args.descs[base + src], lane & 3);
+      if (k < nrec) rewrite_check(args, base + src, rs, *XSKNF_GLD(args.descs + base + src, 16), lane & 3);
     }
     __builtin_amdgcn_wave_barrier();   // `which` is rewritten by the next chunk
   }
