@@ -77,9 +77,9 @@ def parse():
                    help="threads for the all-cores CPU leg (-1 = the process's CPUs, at most 16; 0 = skip)")
     p.add_argument("--min-warmup-s", type=float, default=0.1,
                    help="keep warming up (untimed) until this much time has passed")
-    p.add_argument("--root-scatter", action="store_true",
-                   help="N > 1: also time the distribution of a root-resident global IMIX batch "
-                        "(SURVEY 8(e) collective 1), reported as `root_scatter`")
+    p.add_argument("--no-root-scatter", action="store_true",
+                   help="N > 1: skip the distribution of a root-resident global IMIX batch (SURVEY 8(e) "
+                        "collective 1, reported as `root_scatter`; timed by default when N > 1)")
     p.add_argument("--rotate", type=int, default=0,
                    help="batches the steps cycle through (0 = enough to exceed --rotate-bytes)")
     p.add_argument("--rotate-bytes", type=int, default=1 << 30)
@@ -505,7 +505,17 @@ def main():
         del r
         torch.cuda.empty_cache()
 
-    root_scatter = root_scatter_leg(args, world, rank, dev) if (args.root_scatter and world > 1) else None
+    root_scatter = root_scatter_leg(args, world, rank, dev) if (world > 1 and not args.no_root_scatter) else None
+    # what the collectives saw: every rank contributes 1 (so a SCALE line shows
+    # that the backend really had N ranks), and the frames summed over ranks
+    dist_info = None
+    if world > 1:
+        seen = allreduce_sum_i64([1], world)[0]
+        dist_info = {"ranks_seen": seen, "backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
+                     "frames_allreduced": prim["counters"][0],
+                     "collective_device": coll_device(),
+                     "collectives": "barrier + max-time and counter all-reduces after the timed region; "
+                                    "root_scatter: broadcast + point-to-point isend/irecv"}
 
     total_frames, total_bytes, n_drop, n_fwd = prim["counters"]
     step_s = prim["wall_max"] / args.steps          # wall clock, max over ranks: `value`
@@ -558,6 +568,8 @@ def main():
             out["config"]["rehearsal"] = rehearsal
         if root_scatter is not None:
             out["root_scatter"] = root_scatter
+        if dist_info is not None:
+            out["dist"] = dist_info
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

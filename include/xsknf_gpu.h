@@ -189,12 +189,14 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            the 4-byte records come back and the host writes
  *                            the 2 check bytes.  A batch of frames scattered
  *                            over the UMEM runs as ZEROCOPY instead.
- * One context = one worker thread.  It keeps up to four batches in flight (four slots,
- * each with its own HIP stream): the copies and kernel of one overlap the
- * other's, and the host's share of one overlaps the device's share of the other.
+ * One context = one worker thread.  It keeps up to five batches in flight (five slots,
+ * each with its own HIP stream; XSKNF_MAX_HOOK_DEPTH batches out plus the one being
+ * submitted): the copies and kernel of one overlap another's, and the host's share
+ * of one overlaps the device's share of the others.
  * xsknf_gpu_ctx_process_batch() is synchronous: when it returns, verdicts and
  * check bytes are in host memory (a batch larger than 65536 frames runs as
- * pieces through both slots).  xsknf_gpu_ctx_submit() returns once the batch
+ * pieces through the slots; if a piece fails to start, the pieces already
+ * started are completed before the error returns).  xsknf_gpu_ctx_submit() returns once the batch
  * is enqueued, with a ticket; xsknf_gpu_ctx_wait(ticket) returns once that
  * batch and every earlier one is complete (verdicts written, check bytes in
  * the UMEM).  A submit may itself complete older batches to free a slot.  The

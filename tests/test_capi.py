@@ -119,3 +119,20 @@ def test_launch_shape_for_lengths_without_gpu():
     assert shape(9000, 9000)[3] == 52          # jumbo: 4-chunk window, tile pool, whatever the mean
     assert shape(64, 64)[1] == 1               # lane kernel
     assert lib.xsknf_gpu_launch_cfg_for_lens(1500, 1500, None) == -errno.EINVAL
+
+
+def test_one_hip_runtime_per_process():
+    """Loading the library before torch must not leave two HIP runtimes in the
+    process (ROCm's and torch's bundled one): _lib.load() binds to torch's."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from xsknf_amd import _lib; _lib.load()\n"
+            "import torch\n"
+            "maps = open('/proc/self/maps').read().split('\\n')\n"
+            "hip = sorted({l.split()[-1] for l in maps if 'libamdhip64' in l})\n"
+            "hsa = sorted({l.split()[-1] for l in maps if 'libhsa-runtime64' in l})\n"
+            "print(len(hip), len(hsa))\n") % ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split() == ["1", "1"], out.stdout

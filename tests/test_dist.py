@@ -102,3 +102,62 @@ def test_root_scatter_shards_are_bit_exact(world):
         lo, hi = ranges[r]
         assert v == fv[lo:hi].tolist(), f"rank {r} verdicts"
         assert ub == full[b0:b1].tobytes(), f"rank {r} bytes"
+
+
+class _FakeDist:
+    """Records what scatter_from_root asks of torch.distributed (one process)."""
+
+    class P2POp:
+        def __init__(self, op, tensor, peer):
+            self.op, self.tensor, self.peer = op, tensor, peer
+
+    def __init__(self, meta=None):
+        self.meta = meta
+        self.ops = []
+
+    def isend(self, *a):
+        pass
+
+    def irecv(self, *a):
+        pass
+
+    def broadcast(self, t, src):
+        if self.meta is not None:      # a non-root rank: the root's table arrives
+            t.copy_(self.meta)
+
+    def batch_isend_irecv(self, ops):
+        self.ops = list(ops)
+        return []
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_root_scatter_bookkeeping(world):
+    """The offsets and shapes scatter_from_root hands the backend, independent of
+    where the tensors live (bench.py runs it on HBM tensors over RCCL at N > 1):
+    the root sends each peer a view of exactly its span and an (n, 2) int64
+    descriptor tensor; a peer posts receives of the same sizes into a buffer
+    with 16 spare bytes; the rebased descriptors address the span."""
+    from xsknf_amd.shard import rebase_descs, scatter_from_root, shard_spans
+    b = frames.unaligned_batch(5000, "imix", seed=41)
+    frames.inject_edge_cases(b, 0.05, seed=42)
+    umem = torch.from_numpy(b.umem.copy())
+    ranges = shard_by_bytes(b.descs["len"], world)
+    spans = shard_spans(b.descs, ranges, umem.numel())
+    fd = _FakeDist()
+    lu, ld, (b0, b1) = scatter_from_root(fd, umem, b.descs, ranges, 0, world, "cpu")
+    assert (b0, b1) == spans[0] and lu.data_ptr() == umem.data_ptr() + spans[0][0]
+    assert ld.shape == (ranges[0][1] - ranges[0][0], 2) and ld.dtype == torch.int64
+    sends = [(o.peer, o.tensor) for o in fd.ops]
+    assert [p for p, _ in sends] == [r for r in range(1, world) for _ in (0, 1)]
+    for r in range(1, world):
+        span_t, desc_t = [t for p, t in sends if p == r]
+        (rb0, rb1), (lo, hi) = spans[r], ranges[r]
+        assert span_t.data_ptr() == umem.data_ptr() + rb0 and span_t.numel() == rb1 - rb0
+        want = rebase_descs(b.descs[lo:hi], rb0, umem.numel())
+        assert np.array_equal(desc_t.numpy().view(frames.DESC_DTYPE).reshape(-1), want)
+        # the peer's side: receives sized from the broadcast table
+        meta = torch.tensor([[s0, s1, h - l] for (s0, s1), (l, h) in zip(spans, ranges)], dtype=torch.int64)
+        fp = _FakeDist(meta)
+        pu, pd, (p0, p1) = scatter_from_root(fp, None, None, None, r, world, "cpu")
+        assert (p0, p1) == (rb0, rb1) and pu.numel() == rb1 - rb0 + 16 and pd.shape == (hi - lo, 2)
+        assert [(o.peer, o.tensor.numel()) for o in fp.ops] == [(0, rb1 - rb0), (0, 2 * (hi - lo))]

@@ -158,3 +158,8 @@ def test_bench_gpus_n_starts_its_ranks(dev, clean_ctx):
     assert line["verdicts"]["forward"] == 2 * 65536
     assert line["secondary"]["config4"]["frames"] == 131072
     assert line["roofline"]["frac"] > 0
+    # self-checking multi-rank line: the backend saw both ranks, and the root
+    # distribution ran by default and delivered every frame
+    assert line["dist"]["ranks_seen"] == 2 and line["dist"]["world_size"] == 2
+    assert line["dist"]["frames_allreduced"] == 2 * 65536
+    assert line["root_scatter"]["frames_total"] == 2 * 65536

@@ -54,3 +54,27 @@ def test_library_options_and_defaults():
     cfg, app = R.parse_args(["--iface=ens1f0", "--", "-i", "5", "-c", "DROP"])
     o = parse_command_line(app)
     assert cfg.interfaces[0] == b"ens1f0" and o.csum_iterations == 5 and o.action == ACTION_DROP
+
+
+@pytest.mark.parametrize("argv,msg", [
+    (["-i", "eth0:q"], "ERROR: unknown copy mode 'q'"),                  # src/xsknf.c:800-812
+    (["-i", "eth0", "-M", "TURBO"], "ERROR: unknown working mode TURBO"),  # :845-858
+    (["-i", "eth0", "-w", "0"], "ERROR: Invalid number of workers 0"),     # :859-866
+    ([], "ERROR: at least one interface in required"),                  # :872-874
+    (["-i", "eth0", "-f", "3000"], "--frame-size=3000 is not a power of two"),   # :866-871
+    (["-i", "eth0", "-Z"], "invalid option -- 'Z'"),                      # getopt, then usage()
+])
+def test_library_option_errors_exit_1_with_usage(argv, msg):
+    """xsknf_parse_args ends the process on a bad library option, as the
+    reference's does (usage() + exit(1)); runtime.parse_args therefore runs it
+    in a child process here and checks the exit status and the message."""
+    import subprocess
+    import sys
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from xsknf_amd import runtime as R\n"
+            "R.parse_args(%r)\n"
+            "print('returned')\n") % (root, argv)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 1, (p.returncode, p.stdout, p.stderr)
+    assert msg in p.stderr and "returned" not in p.stdout

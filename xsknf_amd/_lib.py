@@ -85,11 +85,28 @@ class XsknfGpuError(RuntimeError):
 _lib = None
 
 
+def _one_hip_runtime() -> None:
+    """Bind the library to torch's HIP runtime when torch is installed.
+
+    libxsknf_gpu.so needs libamdhip64.so.7 (RUNPATH /opt/rocm).  Loaded after
+    torch, that name resolves to the HIP runtime torch bundles, and the process
+    has one.  Loaded BEFORE torch, it pulls in /opt/rocm's runtime and torch
+    then loads its own (libtorch_hip needs `libamdhip64.so`, a different name):
+    two HIP and two HSA runtimes in one process, where torch.cuda.synchronize()
+    does not wait for this library's launches and torch's stream handles mean
+    nothing to it.  Importing torch first rules that out."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:     # a torch-free process (C tools, the NF binary) has one runtime anyway
+        pass
+
+
 def load() -> ctypes.CDLL:
     """Load the gfx950 library once; raise loudly if it is not built."""
     global _lib
     if _lib is not None:
         return _lib
+    _one_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise XsknfGpuError(
             f"{LIB_PATH} is missing: build it with `make` or __graft_entry__.build(); "

@@ -34,10 +34,13 @@
 //       global_load_lds_dwordx4; R-1 steps stay in flight at no VGPR cost.
 // * Group partial sums reduce with DPP (row_shr / row_bcast) into the group's
 //   last lane.
-// * Stores are two-phase by default: the summing pass never writes the UMEM
-//   (scattered writes mixed into the read stream cost ~25 % of its bandwidth,
-//   tools/hbm_probe), it parks check records in `verdicts`; a write-only
-//   scatter pass then writes the 2 check bytes per frame and the verdicts.
+// * Stores (default_cfg): frames <= 128 B write each check in-line as its
+//   whole 64-byte sector.  Up to 4 KiB every check is deferred -- writes mixed
+//   into the read stream cost several times their bytes (tools/hbm_probe) --
+//   into the wave's LDS patch list (sector index + check); after its last tile
+//   the wave rewrites each listed sector whole (tail_patch_list), with no
+//   second launch.  Jumbo tiles park check records in `verdicts` for a
+//   write-only scatter_checks pass (per-tile policy).
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <mutex>

@@ -7,13 +7,16 @@
 // the GPU instead: host UMEM registered once, then batches submitted with the
 // descriptors and verdicts in host arrays.
 //
-// Two batches are in flight per context: each of the two SLOTS has its own HIP
+// Up to kSlots (5) pieces are in flight per context: each SLOT has its own HIP
 // stream, pinned descriptor / record arrays and staging buffers, so the copies
-// and kernel of one batch overlap the other's, and the host's share of a batch
-// (copy plan, writing the checks) overlaps the device's share of the
-// other.  xsknf_gpu_ctx_submit() / _wait() expose the pipeline; the
-// synchronous xsknf_gpu_ctx_process_batch() cuts a large batch into pieces of
-// kPiece frames and runs them through the same slots.
+// and kernel of one batch overlap another's, and the host's share of a batch
+// (copy plan, writing the checks) overlaps the device's share of the others.
+// Five = the runtime's deepest two-phase hook (XSKNF_MAX_HOOK_DEPTH = 4
+// batches out, include/xsknf.h) plus the batch being submitted, so a worker's
+// submit never waits for its own oldest batch.  xsknf_gpu_ctx_submit() /
+// _wait() expose the pipeline; the synchronous xsknf_gpu_ctx_process_batch()
+// cuts a large batch into pieces of kPiece frames and runs them through the
+// same slots.
 //
 // ZEROCOPY: the UMEM is pinned and mapped into the device address space; the
 //   kernel reads the frames and writes the check bytes over PCIe, in place.
@@ -50,7 +53,7 @@
 
 namespace {
 
-constexpr int kSlots = 4;   // pieces in flight per context (the runtime keeps up to 3 batches out)
+constexpr int kSlots = 5;   // pieces in flight per context: XSKNF_MAX_HOOK_DEPTH (4) batches out + the one submitted
 constexpr uint32_t kPiece = 65536;          // frames per slot submission of process_batch
 constexpr uint64_t kMergeGap = 256;         // frames closer than this share one DMA run
 constexpr size_t kMaxDmaRuns = 8;           // more runs than this (and no 2-D shape): mapped reads
@@ -311,7 +314,13 @@ int submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint32_t i
   for (uint32_t p = 0; p < n; p += c->slot_frames) {
     const uint32_t k = std::min(c->slot_frames, n - p);
     const int rc = submit_piece(c, descs + p, k, ingress_ifindex, opts, verdicts + p);
-    if (rc) return rc;
+    if (rc) {
+      // the batch's earlier pieces are in flight and write into `verdicts` and
+      // the frames: no ticket goes back, so finish them (and anything older)
+      // before the caller recycles those frames
+      if (p) (void)complete_upto(c, c->seq);
+      return rc;
+    }
   }
   if (ticket) *ticket = c->seq;
   return 0;
