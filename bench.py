@@ -80,6 +80,7 @@ def parse():
     p.add_argument("--no-root-scatter", action="store_true",
                    help="N > 1: skip the distribution of a root-resident global IMIX batch (SURVEY 8(e) "
                         "collective 1, reported as `root_scatter`; timed by default when N > 1)")
+    p.add_argument("--no-probes", action="store_true", help="skip the read / step-floor probes")
     p.add_argument("--rotate", type=int, default=0,
                    help="batches the steps cycle through (0 = enough to exceed --rotate-bytes)")
     p.add_argument("--rotate-bytes", type=int, default=1 << 30)
@@ -275,7 +276,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     if cfg.kernel == 1 and cfg.window_chunks & 32:
         family += ", one block per CU, tile pool"
     k_ms = None
-    if primary and args.kernel_steps > 0 and (cfg.fused_stores & 3) != 1:
+    if args.kernel_steps > 0 and (cfg.fused_stores & 3) != 1:
         cfg.fused_stores = 3
         rec = torch.empty(n, dtype=torch.int32, device=dev)
         opts = cs.csum_opts()
@@ -373,7 +374,7 @@ def root_scatter_leg(args, world, rank, dev):
             "layout": "IMIX 64/570/1500 (7:4:1) packed, unaligned-mode descriptors; shards by bytes"}
 
 
-# ---- CPU baseline, attainable read, traffic ------------------------------------
+# ---- CPU baseline, probes, traffic -----------------------------------------------
 
 def cpu_model() -> str:
     try:
@@ -415,48 +416,68 @@ def cpu_baseline(res, budget_s, threads, check=True):
             "gpu_matches_oracle_on_sample": match}
 
 
-def attainable_for(res, reps=20):
-    """the attainable rate of a bare non-temporal read of the same
-    frame bytes (tools/hbm_probe.hip in library form, built by `make tools`), on
-    the batch just measured: uniform aligned frames (chunk stride, data at
-    +256) or a packed (unaligned-mode) UMEM read as one span.  None for mixed
-    lengths in chunks (IMIX) or without the probe library."""
+def probes_for(res, reps=20):
+    """bare memory patterns measured beside the kernels, on the
+    batch just measured (all K rotated batches at once, so the probes read cold
+    bytes too; tools/hbm_probe.hip in library form, built by `make tools`):
+      * read: the fastest bare read of the same frame bytes -- the chunk-stride /
+        packed-span shapes for uniform batches, and for any batch the
+        descriptor-driven shape (each frame's 16-B chunks from its descriptor,
+        64-frame tiles per wave, lanes round robin over the tile's chunks);
+      * step floor: the step's whole memory pattern with no arithmetic -- every
+        frame's bytes read and every check's 64-B sector rewritten (unchanged),
+        in the stream or deferred to each wave's end, whichever is faster.
+    Ratios are probe time / kernel time: < 1 means the kernel is slower than
+    the bare pattern, > 1 that the kernel's own access pattern beats the probe
+    (it does at 1500 B, so there the probe is a reference, not a ceiling)."""
     import ctypes
     path = os.path.join(ROOT, "tools", "build", "libhbm_probe.so")
     if not os.path.exists(path):
         return None
     lens = res["lens"]
-    n = res["n"] * res["K"]          # every rotated batch: the probe reads cold bytes too
-    if res["layout"] == "aligned":
-        if int(lens.min()) != int(lens.max()):
-            return None
-        chunks, stride, off, ln = n, res["chunk"] or frames.CHUNK, frames.HEADROOM, int(lens[0])
-        probe_bytes = n * ((ln + 15) // 16 * 16)
-    else:   # the packed span
-        chunks, stride, off, ln = 1, 0, 0, res["umem"].numel() // 16 * 16
-        probe_bytes = ln
+    K = res["K"]
+    n_all = res["n"] * K
+    umem = res["umem"]
     try:
         lib = ctypes.CDLL(path)
         lib.hbm_probe_read_us.restype = ctypes.c_double
         lib.hbm_probe_read_us.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                           ctypes.c_uint64, ctypes.c_int]
-        torch.cuda.synchronize()
-        us = lib.hbm_probe_read_us(ctypes.c_void_p(res["umem"].data_ptr()), chunks, stride, off, ln, reps)
+        lib.hbm_probe_desc_us.restype = ctypes.c_double
+        lib.hbm_probe_desc_us.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                          ctypes.c_int, ctypes.c_int]
     except (OSError, AttributeError):
         return None
-    if us <= 0:
+    torch.cuda.synchronize()
+    shapes = {}
+    if res["layout"] == "aligned" and int(lens.min()) == int(lens.max()):
+        shapes["chunk_stride"] = lib.hbm_probe_read_us(ctypes.c_void_p(umem.data_ptr()), n_all,
+                                                       res["chunk"] or frames.CHUNK, frames.HEADROOM,
+                                                       int(lens[0]), reps)
+    elif res["layout"] != "aligned":
+        shapes["packed_span"] = lib.hbm_probe_read_us(ctypes.c_void_p(umem.data_ptr()), 1, 0, 0,
+                                                      umem.numel() // 16 * 16, reps)
+    dargs = (ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(res["descs"].data_ptr()), n_all)
+    shapes["descriptors"] = lib.hbm_probe_desc_us(*dargs, 0, reps)
+    shapes = {k: v / K for k, v in shapes.items() if v > 0}
+    if not shapes:
         return None
-    gbs = probe_bytes / us / 1e3
-    us /= res["K"]                    # per batch
-    probe_bytes //= res["K"]
-    out = {"read_GBps": round(gbs, 1), "probe_us": round(us, 2), "probe_bytes": probe_bytes,
-           "probe": "tools/hbm_probe.hip: fastest of its read shapes over the same bytes, nothing written"}
-    k_ms = res["sum_ms"] if res["sum_ms"] is not None else (res["step_ms"] if res["single_kernel"] else None)
+    best = min(shapes, key=shapes.get)
+    us = shapes[best]
+    floors = {k: lib.hbm_probe_desc_us(*dargs, m, reps) / K for k, m in (("in_stream", 1), ("deferred", 2))}
+    floors = {k: v for k, v in floors.items() if v > 0}
+    out = {"read_us": round(us, 2), "read_frame_GBps": round(res["bytes_len"] / us / 1e3, 1),
+           "read_shape": best, "read_shapes_us": {k: round(v, 2) for k, v in shapes.items()},
+           "probe": "tools/hbm_probe.hip: fastest read shape over the same frame bytes, nothing written"}
+    if floors:
+        fb = min(floors, key=floors.get)
+        out["step_floor_us"] = round(floors[fb], 2)
+        out["step_floor_shape"] = fb
+        out["step_floor_shapes_us"] = {k: round(v, 2) for k, v in floors.items()}
+        out["step_vs_floor_probe"] = round(floors[fb] / (res["step_ms"] * 1e3), 4)
+    k_ms = res["sum_ms"] if res["sum_ms"] is not None else None
     if k_ms:
-        # (a single-kernel shape also writes its checks in-line; the probe only reads)
-        k_gbs = res["bytes_len"] / (k_ms / 1e3) / 1e9
-        out["kernel_frame_GBps"] = round(k_gbs, 1)
-        out["kernel_vs_attainable"] = round(k_gbs / gbs, 4)
+        out["summing_kernel_vs_read_probe"] = round(us / (k_ms * 1e3), 4)
     return out
 
 
@@ -482,6 +503,8 @@ def step_summary(r, steps):
            "wall_ms_per_step": round(r["wall_max"] / steps * 1e3, 4), "rotated_batches": r["K"]}
     if r["span"] is not None:
         out["rank0_shard"] = list(r["span"])
+    out["summing_kernel_alone_us"] = round(r["sum_ms"] * 1e3, 2) if r["sum_ms"] is not None else None
+    out["probes"] = r.get("probes")
     out["kernel"] = f"{r['family']} ({r['stores']})"
     out["launch_shape"] = r["shape"]
     out["traffic"] = traffic_for(r["name"])
@@ -501,6 +524,8 @@ def main():
     for name in [s for s in args.secondary.split(",") if s and s != args.workload]:
         r = time_workload(name, args, world, rank, dev, seed, primary=False)
         r["world"] = world
+        if world == 1 and not args.no_probes:
+            r["probes"] = probes_for(r)
         sec[name] = step_summary(r, args.steps)
         del r
         torch.cuda.empty_cache()
@@ -540,7 +565,8 @@ def main():
                      "stream; traffic = FETCH_SIZE/WRITE_SIZE of every kernel of one step",
             "kernels": f"{prim['family']} ({prim['stores']})", "launch_shape": prim["shape"],
             "alg_bytes_per_step": step_alg, "step_us": round(step_k_s * 1e6, 2),
-            "summing_kernel_alone": kernel_alone, "attainable": attainable_for(prim)}
+            "summing_kernel_alone": kernel_alone,
+            "probes": None if args.no_probes else probes_for(prim)}
     cpu = None
     if rank == 0 and prim["sample"] is not None:
         cpu = cpu_baseline(prim, args.cpu_seconds, args.cpu_threads)

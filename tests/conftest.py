@@ -39,3 +39,20 @@ def clean_ctx():
     if FORKSERVER is None:
         pytest.skip("no forkserver on this platform")
     return FORKSERVER
+
+
+@pytest.fixture(autouse=True)
+def _gpu_fault_attribution(request):
+    """After every GPU test: wait for the device, give HIP's event thread a
+    moment, and make one more HIP call, so an asynchronously reported fault
+    (a GPU memory fault reaches HIP through its event thread, after the kernel
+    has ended) fails the test that caused it, not a later one."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import time
+    import torch
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        time.sleep(0.02)
+        torch.zeros(1, device="cuda").cpu()

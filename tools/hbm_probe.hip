@@ -490,6 +490,337 @@ done:
   return best;
 }
 
+// ---- descriptor-driven probes (any mix of lengths, aligned or unaligned UMEM) ----
+//
+// probe_desc: exactly the 16-byte chunks that hold each frame's bytes, read
+// from the descriptors as the checksummer sees them (xdp_desc, unaligned
+// offsets in bits 48..63).  A wave owns 64-frame tiles (tile t = wave + k *
+// waves); the tile's chunk counts are prefix-summed in LDS and the wave's
+// lanes take its chunks round robin (lane j reads chunk j, j + 64, ...; U loads
+// in flight per lane), so every lane is busy whatever the mix and consecutive
+// lanes read consecutive chunks of a frame.  WMODE 1 adds the step's own write
+// pattern: the lanes holding a frame's check sector (the aligned 64 bytes
+// around frame byte 40) store it back unchanged right after loading it;
+// WMODE 2 defers those writes as the summing kernel does: after its last tile
+// the wave re-reads each frame's check sector and stores it back (4 lanes per
+// frame, 16 frames per instruction, two tiles in flight).  Bytes are never
+// changed.  Used by bench.py (roofline.attainable for mixed lengths, and the
+// floor of the whole step's memory pattern).
+__device__ __forceinline__ uint64_t desc_off(uint64_t addr) {
+  return (addr & ((1ull << 48) - 1)) + (addr >> 48);
+}
+
+template <int U, int WMODE>
+__global__ __launch_bounds__(256) void probe_desc(uint8_t *__restrict__ base, uint64_t umem_size,
+                                                  const uint4 *__restrict__ descs, uint32_t n,
+                                                  uint32_t *__restrict__ out) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  __shared__ uint32_t pre[4][65];
+  __shared__ uint64_t cps[4][64];
+  __shared__ int32_t sec_lo[4][64];   // chunk index of the frame's check sector start (-1: none)
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint32_t waves = gridDim.x * 4u;
+  const uint32_t ntiles = (n + 63) / 64;
+  uint32_t acc = 0;
+  const uint32_t w0 = blockIdx.x * 4u + wv;
+  for (uint32_t t = w0; t < ntiles; t += waves) {
+    const uint32_t f = t * 64 + lane;
+    uint32_t nch = 0;
+    uint64_t cp = reinterpret_cast<uintptr_t>(base);
+    int32_t sl = -1;
+    if (f < n) {
+      const uint4 d = descs[f];
+      const uint64_t off = desc_off((static_cast<uint64_t>(d.y) << 32) | d.x);
+      const uint32_t len = d.z;
+      if (off <= umem_size && len <= umem_size - off && len > 0) {
+        const uint64_t fp = reinterpret_cast<uintptr_t>(base) + off;
+        const uint32_t rs = static_cast<uint32_t>(fp & 15);
+        cp = fp - rs;
+        nch = (rs + len + 15) >> 4;
+        const uint64_t sec = (fp + 40) & ~63ull;
+        if (len >= 48 && sec >= fp && sec + 64 <= fp + len) sl = static_cast<int32_t>((sec - cp) >> 4);
+      }
+    }
+    // inclusive scan of the chunk counts
+    uint32_t x = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), o, 64));
+      if (lane >= o) x += y;
+    }
+    pre[wv][lane + 1] = x;
+    if (lane == 0) pre[wv][0] = 0;
+    cps[wv][lane] = cp;
+    sec_lo[wv][lane] = sl;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = pre[wv][64];
+    // lane's first chunk j = lane: its frame by binary search, later ones by walking
+    uint32_t fr = 0;
+    {
+      uint32_t lo = 0, hi = 64;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[wv][mid + 1] <= static_cast<uint32_t>(lane)) lo = mid + 1; else hi = mid;
+      }
+      fr = lo;
+    }
+    for (uint32_t j0 = 0; j0 < total; j0 += 64 * U) {
+      u4v v[U];
+      uint64_t a[U];
+      bool mine[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t j = j0 + lane + 64 * k;
+        const uint32_t jj = j < total ? j : total - 1;
+        while (fr < 63 && pre[wv][fr + 1] <= jj) ++fr;
+        const uint32_t c = jj - pre[wv][fr];
+        a[k] = cps[wv][fr] + 16ull * c;
+        mine[k] = WMODE == 1 && j < total && sec_lo[wv][fr] >= 0 && static_cast<int32_t>(c) >= sec_lo[wv][fr] &&
+                  static_cast<int32_t>(c) < sec_lo[wv][fr] + 4;
+        v[k] = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a[k]));
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+        if (WMODE == 1 && mine[k]) __builtin_nontemporal_store(v[k], reinterpret_cast<u4v *>(a[k]));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (WMODE == 2) {
+    const int piece = lane & 3;
+    for (uint32_t t = w0; t < ntiles; t += 2 * waves) {
+      u4v v[2][4];
+      uint8_t *p[2][4];
+      bool ok[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t f = (t + h * waves) * 64 + 16 * k + (lane >> 2);
+          ok[h][k] = false;
+          p[h][k] = base;
+          if (t + h * waves < ntiles && f < n) {
+            const uint4 d = descs[f];
+            const uint64_t off = desc_off((static_cast<uint64_t>(d.y) << 32) | d.x);
+            const uint32_t len = d.z;
+            if (off <= umem_size && len <= umem_size - off && len >= 48) {
+              uint8_t *fp = base + off;
+              uint8_t *sec = fp + 40 - (reinterpret_cast<uintptr_t>(fp + 40) & 63);
+              ok[h][k] = sec >= fp && sec + 64 <= fp + len;
+              p[h][k] = sec + 16 * piece;
+            }
+          }
+          if (ok[h][k]) v[h][k] = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(p[h][k]));
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (ok[h][k]) __builtin_nontemporal_store(v[h][k], reinterpret_cast<u4v *>(p[h][k]));
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// probe_desc_pool: probe_desc's read (WMODE 0) or deferred rewrite (WMODE 2)
+// with the summing kernel's schedule -- one SW-wave block per CU whose waves
+// draw the block's tiles (every nb-th from the block index) from an LDS
+// counter, so a CU's faster waves take more tiles.
+template <int U, int WMODE, int SW>
+__global__ __launch_bounds__(SW * 64) void probe_desc_pool(uint8_t *__restrict__ base, uint64_t umem_size,
+                                                          const uint4 *__restrict__ descs, uint32_t n,
+                                                          uint32_t *__restrict__ out) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  __shared__ uint32_t pre[SW][65];
+  __shared__ uint64_t cps[SW][64];
+  __shared__ uint32_t next;
+  __shared__ uint32_t mine_tiles[SW][64];   // the wave's tiles, for the deferred rewrites
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nb = gridDim.x;
+  const uint32_t ntiles = (n + 63) / 64;
+  const uint32_t bt = ntiles > blockIdx.x ? (ntiles - blockIdx.x + nb - 1) / nb : 0u;
+  if (threadIdx.x == 0) next = SW;
+  __syncthreads();
+  uint32_t acc = 0, done = 0;
+  for (uint32_t u = wv; u < bt;) {
+    const uint32_t t = blockIdx.x + u * nb;
+    if (WMODE == 2 && done < 64 && lane == 0) mine_tiles[wv][done] = t;
+    ++done;
+    uint32_t dq = 0;
+    if (lane == 0) dq = __hip_atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t un = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dq), 0));
+    const uint32_t f = t * 64 + lane;
+    uint32_t nch = 0;
+    uint64_t cp = reinterpret_cast<uintptr_t>(base);
+    if (f < n) {
+      const uint4 d = descs[f];
+      const uint64_t off = desc_off((static_cast<uint64_t>(d.y) << 32) | d.x);
+      const uint32_t len = d.z;
+      if (off <= umem_size && len <= umem_size - off && len > 0) {
+        const uint64_t fp = reinterpret_cast<uintptr_t>(base) + off;
+        const uint32_t rs = static_cast<uint32_t>(fp & 15);
+        cp = fp - rs;
+        nch = (rs + len + 15) >> 4;
+      }
+    }
+    uint32_t x = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), o, 64));
+      if (lane >= o) x += y;
+    }
+    pre[wv][lane + 1] = x;
+    if (lane == 0) pre[wv][0] = 0;
+    cps[wv][lane] = cp;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = pre[wv][64];
+    uint32_t fr = 0;
+    {
+      uint32_t lo = 0, hi = 64;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[wv][mid + 1] <= static_cast<uint32_t>(lane)) lo = mid + 1; else hi = mid;
+      }
+      fr = lo;
+    }
+    for (uint32_t j0 = 0; j0 < total; j0 += 64 * U) {
+      u4v v[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t j = j0 + lane + 64 * k;
+        const uint32_t jj = j < total ? j : total - 1;
+        while (fr < 63 && pre[wv][fr + 1] <= jj) ++fr;
+        v[k] = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(cps[wv][fr] + 16ull * (jj - pre[wv][fr])));
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    u = un;
+  }
+  if (WMODE == 2) {
+    const int piece = lane & 3;
+    const uint32_t nt = done < 64 ? done : 64;
+    for (uint32_t i = 0; i < nt; i += 2) {
+      u4v v[2][4];
+      uint8_t *p[2][4];
+      bool ok[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          ok[h][k] = false;
+          p[h][k] = base;
+          if (i + h < nt) {
+            const uint32_t f = mine_tiles[wv][i + h] * 64 + 16 * k + (lane >> 2);
+            if (f < n) {
+              const uint4 d = descs[f];
+              const uint64_t off = desc_off((static_cast<uint64_t>(d.y) << 32) | d.x);
+              const uint32_t len = d.z;
+              if (off <= umem_size && len <= umem_size - off && len >= 48) {
+                uint8_t *fp = base + off;
+                uint8_t *sec = fp + 40 - (reinterpret_cast<uintptr_t>(fp + 40) & 63);
+                ok[h][k] = sec >= fp && sec + 64 <= fp + len;
+                p[h][k] = sec + 16 * piece;
+              }
+            }
+          }
+          if (ok[h][k]) v[h][k] = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(p[h][k]));
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (ok[h][k]) __builtin_nontemporal_store(v[h][k], reinterpret_cast<u4v *>(p[h][k]));
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// The fastest probe_desc shape (U = 4 / 8 loads in flight per lane, 2 / 4 / 8
+// blocks per CU) over `n` descriptors of an existing device batch, averaged
+// over `reps` launches after 3 warm-ups on the null stream: wmode 0 reads
+// only; 1 / 2 add the check-sector rewrites (in the stream / deferred to the
+// wave's end).  Microseconds, or a negative value on a HIP error.
+extern "C" __attribute__((visibility("default"))) double hbm_probe_desc_us(void *base, uint64_t umem_size,
+                                                                          const void *descs, uint32_t n,
+                                                                          int wmode, int reps) {
+  uint32_t *out = nullptr;
+  if (n == 0 || hipMalloc(&out, 4) != hipSuccess) return -1.0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 256;
+  typedef void (*kfn)(uint8_t *, uint64_t, const uint4 *, uint32_t, uint32_t *);
+  const kfn k0[] = {probe_desc<4, 0>, probe_desc<8, 0>};
+  const kfn k1[] = {probe_desc<4, 1>, probe_desc<8, 1>};
+  const kfn k2[] = {probe_desc<4, 2>, probe_desc<8, 2>};
+  const kfn *ks = wmode == 1 ? k1 : (wmode == 2 ? k2 : k0);
+  const int grids[] = {2, 4, 8};
+  const bool verbose = getenv("HBM_PROBE_VERBOSE") != nullptr;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  double best = -1.0;
+  uint8_t *b = static_cast<uint8_t *>(base);
+  const uint4 *d = static_cast<const uint4 *>(descs);
+  for (int s = 0; s < 2 && best != -2.0; ++s) {
+    for (int g : grids) {
+      const uint32_t need = ((n + 63) / 64 + 3) / 4;
+      const uint32_t grid = need < static_cast<uint32_t>(cus * g) ? need : static_cast<uint32_t>(cus * g);
+      for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(ks[s], dim3(grid), dim3(256), 0, 0, b, umem_size, d, n, out);
+      (void)hipEventRecord(e0);
+      for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(ks[s], dim3(grid), dim3(256), 0, 0, b, umem_size, d, n, out);
+      (void)hipEventRecord(e1);
+      float ms = -1.0f;
+      if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+        best = -2.0;
+        break;
+      }
+      const double us = ms * 1e3 / reps;
+      if (verbose) fprintf(stderr, "hbm_probe desc wmode %d U %d grid %d/CU: %.2f us\n", wmode, s ? 8 : 4, g, us);
+      if (best < 0 || us < best) best = us;
+    }
+  }
+  // the summing kernel's schedule: one 8 / 12 / 16-wave block per CU, tiles from an LDS pool
+  if (best != -2.0 && wmode != 1) {
+    struct PoolShape { kfn k; int sw; };
+    const PoolShape ps[] = {
+        {wmode == 2 ? probe_desc_pool<4, 2, 8> : probe_desc_pool<4, 0, 8>, 8},
+        {wmode == 2 ? probe_desc_pool<4, 2, 12> : probe_desc_pool<4, 0, 12>, 12},
+        {wmode == 2 ? probe_desc_pool<4, 2, 16> : probe_desc_pool<4, 0, 16>, 16},
+        {wmode == 2 ? probe_desc_pool<8, 2, 8> : probe_desc_pool<8, 0, 8>, 8},
+        {wmode == 2 ? probe_desc_pool<8, 2, 12> : probe_desc_pool<8, 0, 12>, 12},
+    };
+    for (const PoolShape &q : ps) {
+      int bpc = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, q.k, q.sw * 64, 0) != hipSuccess || bpc < 1) {
+        (void)hipGetLastError();
+        continue;
+      }
+      for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(q.k, dim3(cus), dim3(q.sw * 64), 0, 0, b, umem_size, d, n, out);
+      (void)hipEventRecord(e0);
+      for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(q.k, dim3(cus), dim3(q.sw * 64), 0, 0, b, umem_size, d, n, out);
+      (void)hipEventRecord(e1);
+      float ms = -1.0f;
+      if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+        best = -2.0;
+        break;
+      }
+      const double us = ms * 1e3 / reps;
+      if (verbose) fprintf(stderr, "hbm_probe desc-pool wmode %d SW %d: %.2f us\n", wmode, q.sw, us);
+      if (best < 0 || us < best) best = us;
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(out);
+  return best;
+}
+
 #ifndef HBM_PROBE_LIB
 int main(int argc, char **argv) {
   if (argc < 5) { fprintf(stderr, "usage: %s chunks stride off len [reps]\n", argv[0]); return 2; }
