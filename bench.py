@@ -425,8 +425,9 @@ def probes_for(res, reps=20):
         descriptor-driven shape (each frame's 16-B chunks from its descriptor,
         64-frame tiles per wave, lanes round robin over the tile's chunks);
       * step floor: the step's whole memory pattern with no arithmetic -- every
-        frame's bytes read and every check's 64-B sector rewritten (unchanged),
-        in the stream or deferred to each wave's end, whichever is faster.
+        frame's bytes read, every check's 64-B sector rewritten (unchanged) in
+        the stream or deferred to each wave's end, whichever is faster, and a
+        4-byte verdict written per frame.
     Ratios are probe time / kernel time: < 1 means the kernel is slower than
     the bare pattern, > 1 that the kernel's own access pattern beats the probe
     (it does at 1500 B, so there the probe is a reference, not a ceiling)."""
@@ -464,13 +465,16 @@ def probes_for(res, reps=20):
         return None
     best = min(shapes, key=shapes.get)
     us = shapes[best]
-    floors = {k: lib.hbm_probe_desc_us(*dargs, m, reps) / K for k, m in (("in_stream", 1), ("deferred", 2))}
+    # the step writes a 4-byte verdict per frame as well (modes 3 / 4); 1 / 2 without it, for reference
+    floors = {k: lib.hbm_probe_desc_us(*dargs, m, reps) / K
+              for k, m in (("in_stream", 3), ("deferred", 4), ("in_stream_no_verdicts", 1),
+                           ("deferred_no_verdicts", 2))}
     floors = {k: v for k, v in floors.items() if v > 0}
     out = {"read_us": round(us, 2), "read_frame_GBps": round(res["bytes_len"] / us / 1e3, 1),
            "read_shape": best, "read_shapes_us": {k: round(v, 2) for k, v in shapes.items()},
            "probe": "tools/hbm_probe.hip: fastest read shape over the same frame bytes, nothing written"}
     if floors:
-        fb = min(floors, key=floors.get)
+        fb = min((k for k in floors if "no_verdicts" not in k), key=floors.get, default=min(floors, key=floors.get))
         out["step_floor_us"] = round(floors[fb], 2)
         out["step_floor_shape"] = fb
         out["step_floor_shapes_us"] = {k: round(v, 2) for k, v in floors.items()}

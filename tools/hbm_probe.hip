@@ -514,6 +514,9 @@ template <int U, int WMODE>
 __global__ __launch_bounds__(256) void probe_desc(uint8_t *__restrict__ base, uint64_t umem_size,
                                                   const uint4 *__restrict__ descs, uint32_t n,
                                                   uint32_t *__restrict__ out) {
+  // WMODE 3 / 4 = 1 / 2 plus a 4-byte verdict per frame (one 256-byte store per
+  // tile), into `out` + 1 (a buffer of n + 1 words)
+  constexpr int WM = WMODE >= 3 ? WMODE - 2 : WMODE;
   typedef uint32_t u4v __attribute__((ext_vector_type(4)));
   __shared__ uint32_t pre[4][65];
   __shared__ uint64_t cps[4][64];
@@ -576,19 +579,20 @@ __global__ __launch_bounds__(256) void probe_desc(uint8_t *__restrict__ base, ui
         while (fr < 63 && pre[wv][fr + 1] <= jj) ++fr;
         const uint32_t c = jj - pre[wv][fr];
         a[k] = cps[wv][fr] + 16ull * c;
-        mine[k] = WMODE == 1 && j < total && sec_lo[wv][fr] >= 0 && static_cast<int32_t>(c) >= sec_lo[wv][fr] &&
+        mine[k] = WM == 1 && j < total && sec_lo[wv][fr] >= 0 && static_cast<int32_t>(c) >= sec_lo[wv][fr] &&
                   static_cast<int32_t>(c) < sec_lo[wv][fr] + 4;
         v[k] = __builtin_nontemporal_load(reinterpret_cast<const u4v *>(a[k]));
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
-        if (WMODE == 1 && mine[k]) __builtin_nontemporal_store(v[k], reinterpret_cast<u4v *>(a[k]));
+        if (WM == 1 && mine[k]) __builtin_nontemporal_store(v[k], reinterpret_cast<u4v *>(a[k]));
       }
     }
+    if (WMODE >= 3 && f < n) out[1 + f] = acc;
     __builtin_amdgcn_wave_barrier();
   }
-  if (WMODE == 2) {
+  if (WM == 2) {
     const int piece = lane & 3;
     for (uint32_t t = w0; t < ntiles; t += 2 * waves) {
       u4v v[2][4];
@@ -751,14 +755,16 @@ extern "C" __attribute__((visibility("default"))) double hbm_probe_desc_us(void 
                                                                           const void *descs, uint32_t n,
                                                                           int wmode, int reps) {
   uint32_t *out = nullptr;
-  if (n == 0 || hipMalloc(&out, 4) != hipSuccess) return -1.0;
+  if (n == 0 || hipMalloc(&out, 4ull * (n + 1)) != hipSuccess) return -1.0;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) cus = 256;
   typedef void (*kfn)(uint8_t *, uint64_t, const uint4 *, uint32_t, uint32_t *);
   const kfn k0[] = {probe_desc<4, 0>, probe_desc<8, 0>};
   const kfn k1[] = {probe_desc<4, 1>, probe_desc<8, 1>};
   const kfn k2[] = {probe_desc<4, 2>, probe_desc<8, 2>};
-  const kfn *ks = wmode == 1 ? k1 : (wmode == 2 ? k2 : k0);
+  const kfn k3[] = {probe_desc<4, 3>, probe_desc<8, 3>};
+  const kfn k4[] = {probe_desc<4, 4>, probe_desc<8, 4>};
+  const kfn *ks = wmode == 1 ? k1 : (wmode == 2 ? k2 : (wmode == 3 ? k3 : (wmode == 4 ? k4 : k0)));
   const int grids[] = {2, 4, 8};
   const bool verbose = getenv("HBM_PROBE_VERBOSE") != nullptr;
   hipEvent_t e0, e1;
@@ -786,7 +792,7 @@ extern "C" __attribute__((visibility("default"))) double hbm_probe_desc_us(void 
     }
   }
   // the summing kernel's schedule: one 8 / 12 / 16-wave block per CU, tiles from an LDS pool
-  if (best != -2.0 && wmode != 1) {
+  if (best != -2.0 && (wmode == 0 || wmode == 2)) {
     struct PoolShape { kfn k; int sw; };
     const PoolShape ps[] = {
         {wmode == 2 ? probe_desc_pool<4, 2, 8> : probe_desc_pool<4, 0, 8>, 8},

@@ -761,8 +761,9 @@ constexpr uint32_t kNoTile = 0xffffffffu;   // no tile / unit
 // block index, are a pool its waves claim from through an LDS counter, one
 // tile ahead, as the split kernel's pool (a CU's waves do not stream equally
 // fast; from a shared pool the faster ones take more tiles).
-template <int NCH, int SPT, int SW = kWavesPerBlock>
-__global__ __launch_bounds__(SW * kWave) void checksum_kernel_lane(const KernelArgs args) {
+template <int NCH, int SPT, int SW = kWavesPerBlock, int WPE = 1>
+__global__ __launch_bounds__(SW * kWave) __attribute__((amdgpu_waves_per_eu(WPE)))
+void checksum_kernel_lane(const KernelArgs args) {
   constexpr uint32_t T = SPT * kWave;        // frames per tile
   constexpr bool kPool = SW > kWavesPerBlock;
   __shared__ __attribute__((aligned(16))) uint8_t hdr[SW][kWave][kLaneSlot];
@@ -1644,6 +1645,120 @@ void checksum_kernel_split(const KernelArgs args) {
 }
 
 #ifdef XSKNF_AB
+// ---- small-frame kernel (A/B: frames of at most 64 B, BASELINE config 2) --------
+//
+// Occupancy over per-wave overlap: a frame of <= 64 B is one 64-byte sector at
+// a 2 KiB stride, so the step is bound by how many such sectors are in flight,
+// not by bytes.  Each wave takes a tile of 64 frames: its 4 window loads are
+// transposed (lanes 4i .. 4i+3 read frame 16p + i's four 16-byte chunks, one
+// coalesced 64-byte request per frame) into a 64-byte LDS slot per frame; lane
+// l then parses, sums and finishes frame l from its slot, patches its check into
+// the slot and the wave writes each check's sector back whole, 16 frames per
+// store (4 lanes each), right after reading it.  4 KiB of LDS and <= 64 VGPRs
+// per wave: 8 waves per SIMD.  Frames longer than the window read their other
+// chunks lane by lane (any length is correct; hint > 64 picks another kernel).
+template <int SW>
+__global__ __launch_bounds__(SW * kWave) __attribute__((amdgpu_waves_per_eu(8)))
+void checksum_kernel_small(const KernelArgs args) {
+  constexpr int kWin = 4;                               // window chunks (64 B)
+  __shared__ __attribute__((aligned(16))) uint8_t win[SW][kWave * 16 * kWin];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t area = lds_addr(&win[wv][0]);
+  const uint32_t slot = area + 16 * kWin * lane;
+  const uint32_t waves = gridDim.x * SW;
+  const uint32_t last = args.n - 1;
+  const uint32_t ntiles = (args.n + kWave - 1) / kWave;
+  uint32_t tile = blockIdx.x * SW + wv;
+  const auto desc_at = [&](uint32_t t) {
+    return *XSKNF_GLD(reinterpret_cast<const uint4 *>(args.descs + (t < ntiles ? min(t * kWave + lane, last) : last)), 16);
+  };
+  uint4 d = desc_at(tile);
+  for (; tile < ntiles; tile += waves) {
+    const uint4 dn = desc_at(tile + waves);
+    const uint32_t f = tile * kWave + lane;
+    const FrameRef r = lane_ref(args, d, f);
+    // transposed window: instruction p, lane L -> chunk L % 4 of frame 16 p + L / 4
+    {
+      const uintptr_t cpv = reinterpret_cast<uintptr_t>(r.cp);
+      uint4 x[kWin];
+#pragma unroll
+      for (int p = 0; p < kWin; ++p) {
+        const int g = 16 * p + lane / 4;
+        const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv)));
+        const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
+        const int nc = __builtin_amdgcn_ds_bpermute(g << 2, r.nch);
+        const gchunk_ptr cp = reinterpret_cast<gchunk_ptr>((static_cast<uintptr_t>(hi) << 32) | lo);
+        const u32x4 y = *XSKNF_GLD(cp + min(lane % 4, nc - 1), 16);
+        x[p] = make_uint4(y.x, y.y, y.z, y.w);
+      }
+      compiler_barrier();
+#pragma unroll
+      for (int p = 0; p < kWin; ++p) lds_store_u128(area + 16 * kWin * (16 * p + lane / 4) + 16 * (lane % 4), x[p]);
+      compiler_barrier();
+    }
+    // header: every field but the UDP length / old check lies in the window
+    // (rs <= 15); those 4 bytes come from the frame itself when the header is
+    // longer than the window (large ihl)
+    const uint32_t hb = slot + r.rs;
+    Header h;
+    {
+      const uint32_t w12 = lds_u32(hb + 12), w20 = lds_u32(hb + 20), w24 = lds_u32(hb + 24);
+      const uint32_t w28 = lds_u32(hb + 28), w32 = lds_u32(hb + 32);
+      h.u = 14 + 4 * ((w12 >> 16) & 0x0f);
+      uint32_t wu = 0;
+      if (r.rs + h.u + 8 <= 16 * kWin) {
+        wu = lds_u32(hb + h.u + 4);
+      } else if (r.live && h.u + 8 <= r.len) {
+        const uint8_t *q = XSKNF_GLD(r.fp + h.u + 4, 4);
+        wu = q[0] | (static_cast<uint32_t>(q[1]) << 8) | (static_cast<uint32_t>(q[2]) << 16) |
+             (static_cast<uint32_t>(q[3]) << 24);
+      }
+      h.ipv4 = (w12 & 0xffffu) == 0x0008u;
+      h.udp = (w20 >> 24) == 17u;
+      h.pseudo = (w24 >> 16) + (w28 & 0xffffu) + (w28 >> 16) + (w32 & 0xffffu) + 0x1100u + (wu & 0xffffu);
+      h.old_check = wu >> 16;
+    }
+    bool do_sum;
+    const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
+    LaneOut o = {r.exists ? verdict : 0, false, slot, r.fp};
+    if (do_sum) {
+      const int lo = r.rs + h.u, hi = r.rs + r.len;
+      const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
+      const uint32_t wh = wl << 8 | wl >> 24;
+      uint32_t acc_lo = 0, acc_hi = 0;
+#pragma unroll
+      for (int k = 0; k < kWin; ++k) chunk_sum(lds_u128(slot + 16 * k), 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
+      for (int k = kWin; k < r.nch; ++k)
+        chunk_sum(*XSKNF_GLD(r.cp + k, 16), 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
+      const uint16_t c = check_of(h, acc_lo + (acc_hi << 8), args.payload_mult);
+      const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
+      const uintptr_t ck = f0 + h.u + 6;
+      const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
+      const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
+      if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
+          sec + 64 <= c0 + 16 * kWin) {
+        const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
+        lds_store_u8(at, static_cast<uint8_t>(c));
+        lds_store_u8(at + 1, static_cast<uint8_t>(c >> 8));
+        o.sector = true;
+        o.lds_sec = slot + static_cast<uint32_t>(sec - c0);
+        o.gsec = r.fp + static_cast<intptr_t>(sec - f0);
+      } else {
+        XSKNF_GST(r.fp + h.u + 6, 2) *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
+      }
+    }
+    store_sectors(o, lane, args.plain_sector);
+    if (f < args.n) {
+      XSKNF_GST(args.verdicts + f, 4) args.verdicts[f] = o.res;
+    }
+    compiler_barrier();   // the next tile rewrites the slots
+    d = dn;
+  }
+}
+#endif  // XSKNF_AB
+
+#ifdef XSKNF_AB
 // ---- LDS-DMA ring kernel ------------------------------------------------------
 //
 // Each wave streams its steps (G frames, one per group) through a private ring
@@ -2005,9 +2120,9 @@ int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel launch");
 }
 
-template <int NCH, int SPT, int SW = kWavesPerBlock>
+template <int NCH, int SPT, int SW = kWavesPerBlock, int WPE = 1>
 int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  auto k = checksum_kernel_lane<NCH, SPT, SW>;
+  auto k = checksum_kernel_lane<NCH, SPT, SW, WPE>;
   if constexpr (SW > kWavesPerBlock) {   // as launch_split: a CU-sized block the device cannot hold
     static thread_local int fits = -1;
     if (fits < 0) {
@@ -2042,6 +2157,16 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
 }
 
 #ifdef XSKNF_AB
+template <int SW>
+int launch_small(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
+  auto k = checksum_kernel_small<SW>;
+  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave, SW)), dim3(SW * kWave), 0, stream, a);
+  return finish_launch(a, stream, "checksum_kernel_small launch");
+}
+#endif
+
+
+#ifdef XSKNF_AB
 template <int LPF, int NCH, int R>
 int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   auto k = checksum_kernel_dma<LPF, NCH, R>;
@@ -2063,6 +2188,8 @@ struct Variant {
 #define XSKNF_L(N, S) {1, N, S, 0, &launch_lane<N, S>}
 // lane kernel, one 16-wave block per CU with the tile pool (window field 32)
 #define XSKNF_LP(N, S) {1, N, S, 0, &launch_lane<N, S, 16>, XSKNF_GPU_KERNEL_AUTO, 32}
+// (A/B) lane kernel held to WPE waves per SIMD (window field 64 + 256 * WPE)
+#define XSKNF_LW(N, S, WPE) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, WPE>, XSKNF_GPU_KERNEL_AUTO, 64 + 256 * WPE}
 #define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
 // split: window field = W, + 16 for the transposed (coalesced) window load
 #define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL, false>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
@@ -2098,6 +2225,10 @@ const Variant kVariants[] = {
     XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
     XSKNF_SP(16, 2, 2), XSKNF_SP(16, 3, 1),         // window prefetch: +3-6 us on 1500 / IMIX / 570 (tune_pfw)
     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
+    XSKNF_L(4, 1),     XSKNF_L(4, 2),     XSKNF_L(5, 1),   // fewer VGPRs, more waves (r03 64 B A/B)
+    XSKNF_LW(4, 1, 8), XSKNF_LW(4, 2, 6), XSKNF_LW(5, 2, 6), XSKNF_LW(5, 1, 8),
+    // small-frame kernel, 8 waves per SIMD (window field 128): 64 B 61.5-62.7 vs the lane kernel's 59.4-60.0 us
+    {1, 4, 1, 0, &launch_small<4>, XSKNF_GPU_KERNEL_AUTO, 128},
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
     XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
@@ -2110,6 +2241,7 @@ const Variant kVariants[] = {
 #undef XSKNF_V
 #undef XSKNF_L
 #undef XSKNF_LP
+#undef XSKNF_LW
 #undef XSKNF_D
 #undef XSKNF_S
 #undef XSKNF_SD
@@ -2126,7 +2258,7 @@ const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
           v.window == c.window_chunks && v.ring == c.lds_ring)
         return &v;
     } else if (v.lpf == c.lanes_per_frame && v.nch == c.chunks_per_lane && v.ring == c.lds_ring &&
-               (c.lds_ring || v.u == c.frames_per_group) && v.window == (c.window_chunks & 32)) {
+               (c.lds_ring || v.u == c.frames_per_group) && v.window == (c.window_chunks & ~31)) {
       return &v;
     }
   }
