@@ -446,12 +446,16 @@ def probes_for(res, reps=20):
                                           ctypes.c_uint64, ctypes.c_int]
         lib.hbm_probe_desc_us.restype = ctypes.c_double
         lib.hbm_probe_desc_us.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
-                                          ctypes.c_int, ctypes.c_int]
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
     except (OSError, AttributeError):
         return None
     torch.cuda.synchronize()
     shapes = {}
-    if res["layout"] == "aligned" and int(lens.min()) == int(lens.max()):
+    # (the chunk-stride and span shapes read everything in one launch: only for
+    # unrotated batches, where that is one batch per launch as the kernels run)
+    if K > 1:
+        pass
+    elif res["layout"] == "aligned" and int(lens.min()) == int(lens.max()):
         shapes["chunk_stride"] = lib.hbm_probe_read_us(ctypes.c_void_p(umem.data_ptr()), n_all,
                                                        res["chunk"] or frames.CHUNK, frames.HEADROOM,
                                                        int(lens[0]), reps)
@@ -459,14 +463,16 @@ def probes_for(res, reps=20):
         shapes["packed_span"] = lib.hbm_probe_read_us(ctypes.c_void_p(umem.data_ptr()), 1, 0, 0,
                                                       umem.numel() // 16 * 16, reps)
     dargs = (ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(res["descs"].data_ptr()), n_all)
-    shapes["descriptors"] = lib.hbm_probe_desc_us(*dargs, 0, reps)
+    # one launch per batch of at most 1M frames, as the kernels run (launch gaps and ramps included)
+    per = min(res["n"], 1 << 20)
+    shapes["descriptors"] = lib.hbm_probe_desc_us(*dargs, 0, reps, per)
     shapes = {k: v / K for k, v in shapes.items() if v > 0}
     if not shapes:
         return None
     best = min(shapes, key=shapes.get)
     us = shapes[best]
     # the step writes a 4-byte verdict per frame as well (modes 3 / 4); 1 / 2 without it, for reference
-    floors = {k: lib.hbm_probe_desc_us(*dargs, m, reps) / K
+    floors = {k: lib.hbm_probe_desc_us(*dargs, m, reps, per) / K
               for k, m in (("in_stream", 3), ("deferred", 4), ("in_stream_no_verdicts", 1),
                            ("deferred_no_verdicts", 2))}
     floors = {k: v for k, v in floors.items() if v > 0}

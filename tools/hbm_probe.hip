@@ -751,9 +751,13 @@ __global__ __launch_bounds__(SW * 64) void probe_desc_pool(uint8_t *__restrict__
 // over `reps` launches after 3 warm-ups on the null stream: wmode 0 reads
 // only; 1 / 2 add the check-sector rewrites (in the stream / deferred to the
 // wave's end).  Microseconds, or a negative value on a HIP error.
+// Launches cover `per_launch` descriptors each (0: all n in one launch), as the
+// kernels' launches do -- a step of a 1M-frame batch pays its launch gap and
+// ramp as the probe must; the time returned is for all n descriptors.
 extern "C" __attribute__((visibility("default"))) double hbm_probe_desc_us(void *base, uint64_t umem_size,
                                                                           const void *descs, uint32_t n,
-                                                                          int wmode, int reps) {
+                                                                          int wmode, int reps,
+                                                                          uint32_t per_launch) {
   uint32_t *out = nullptr;
   if (n == 0 || hipMalloc(&out, 4ull * (n + 1)) != hipSuccess) return -1.0;
   int cus = 0;
@@ -775,11 +779,16 @@ extern "C" __attribute__((visibility("default"))) double hbm_probe_desc_us(void 
   const uint4 *d = static_cast<const uint4 *>(descs);
   for (int s = 0; s < 2 && best != -2.0; ++s) {
     for (int g : grids) {
-      const uint32_t need = ((n + 63) / 64 + 3) / 4;
+      const uint32_t pl = per_launch ? per_launch : n;
+      const uint32_t need = ((pl + 63) / 64 + 3) / 4;
       const uint32_t grid = need < static_cast<uint32_t>(cus * g) ? need : static_cast<uint32_t>(cus * g);
-      for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(ks[s], dim3(grid), dim3(256), 0, 0, b, umem_size, d, n, out);
+      const auto pass = [&]() {
+        for (uint32_t o = 0; o < n; o += pl)
+          hipLaunchKernelGGL(ks[s], dim3(grid), dim3(256), 0, 0, b, umem_size, d + o, n - o < pl ? n - o : pl, out);
+      };
+      for (int w = 0; w < 3; ++w) pass();
       (void)hipEventRecord(e0);
-      for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(ks[s], dim3(grid), dim3(256), 0, 0, b, umem_size, d, n, out);
+      for (int r = 0; r < reps; ++r) pass();
       (void)hipEventRecord(e1);
       float ms = -1.0f;
       if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
@@ -807,9 +816,14 @@ extern "C" __attribute__((visibility("default"))) double hbm_probe_desc_us(void 
         (void)hipGetLastError();
         continue;
       }
-      for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(q.k, dim3(cus), dim3(q.sw * 64), 0, 0, b, umem_size, d, n, out);
+      const uint32_t pl = per_launch ? per_launch : n;
+      const auto pass = [&]() {
+        for (uint32_t o = 0; o < n; o += pl)
+          hipLaunchKernelGGL(q.k, dim3(cus), dim3(q.sw * 64), 0, 0, b, umem_size, d + o, n - o < pl ? n - o : pl, out);
+      };
+      for (int w = 0; w < 3; ++w) pass();
       (void)hipEventRecord(e0);
-      for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(q.k, dim3(cus), dim3(q.sw * 64), 0, 0, b, umem_size, d, n, out);
+      for (int r = 0; r < reps; ++r) pass();
       (void)hipEventRecord(e1);
       float ms = -1.0f;
       if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {

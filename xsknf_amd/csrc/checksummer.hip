@@ -1657,7 +1657,10 @@ void checksum_kernel_split(const KernelArgs args) {
 // store (4 lanes each), right after reading it.  4 KiB of LDS and <= 64 VGPRs
 // per wave: 8 waves per SIMD.  Frames longer than the window read their other
 // chunks lane by lane (any length is correct; hint > 64 picks another kernel).
-template <int SW>
+// MODE (timing experiments only, wrong output): 1 = no parse / sum, the
+// loaded sector is written back as read; 2 = also no LDS: the window
+// registers are stored straight back (the hbm_probe in-stream shape).
+template <int SW, bool NT, int MODE = 0>
 __global__ __launch_bounds__(SW * kWave) __attribute__((amdgpu_waves_per_eu(8)))
 void checksum_kernel_small(const KernelArgs args) {
   constexpr int kWin = 4;                               // window chunks (64 B)
@@ -1689,13 +1692,38 @@ void checksum_kernel_small(const KernelArgs args) {
         const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
         const int nc = __builtin_amdgcn_ds_bpermute(g << 2, r.nch);
         const gchunk_ptr cp = reinterpret_cast<gchunk_ptr>((static_cast<uintptr_t>(hi) << 32) | lo);
-        const u32x4 y = *XSKNF_GLD(cp + min(lane % 4, nc - 1), 16);
-        x[p] = make_uint4(y.x, y.y, y.z, y.w);
+        if constexpr (NT) {
+          x[p] = load_nt(cp + min(lane % 4, nc - 1));
+        } else {
+          const u32x4 y = *XSKNF_GLD(cp + min(lane % 4, nc - 1), 16);
+          x[p] = make_uint4(y.x, y.y, y.z, y.w);
+        }
+      }
+      if constexpr (MODE == 2) {
+#pragma unroll
+        for (int p = 0; p < kWin; ++p) {
+          const int g = 16 * p + lane / 4;
+          const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv)));
+          const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
+          uint8_t *cp = reinterpret_cast<uint8_t *>((static_cast<uintptr_t>(hi) << 32) | lo);
+          store_nt16(cp + 16 * (lane % 4), x[p]);
+        }
+        if (f < args.n) args.verdicts[f] = 0;
+        d = dn;
+        continue;
       }
       compiler_barrier();
 #pragma unroll
       for (int p = 0; p < kWin; ++p) lds_store_u128(area + 16 * kWin * (16 * p + lane / 4) + 16 * (lane % 4), x[p]);
       compiler_barrier();
+    }
+    if constexpr (MODE == 1) {
+      LaneOut o1 = {0, r.live && r.rs == 0 && r.len >= 64, slot, r.fp};
+      store_sectors(o1, lane, false);
+      if (f < args.n) args.verdicts[f] = 0;
+      compiler_barrier();
+      d = dn;
+      continue;
     }
     // header: every field but the UDP length / old check lies in the window
     // (rs <= 15); those 4 bytes come from the frame itself when the header is
@@ -2157,9 +2185,9 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
 }
 
 #ifdef XSKNF_AB
-template <int SW>
+template <int SW, bool NT, int MODE = 0>
 int launch_small(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  auto k = checksum_kernel_small<SW>;
+  auto k = checksum_kernel_small<SW, NT, MODE>;
   hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave, SW)), dim3(SW * kWave), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_small launch");
 }
@@ -2228,7 +2256,10 @@ const Variant kVariants[] = {
     XSKNF_L(4, 1),     XSKNF_L(4, 2),     XSKNF_L(5, 1),   // fewer VGPRs, more waves (r03 64 B A/B)
     XSKNF_LW(4, 1, 8), XSKNF_LW(4, 2, 6), XSKNF_LW(5, 2, 6), XSKNF_LW(5, 1, 8),
     // small-frame kernel, 8 waves per SIMD (window field 128): 64 B 61.5-62.7 vs the lane kernel's 59.4-60.0 us
-    {1, 4, 1, 0, &launch_small<4>, XSKNF_GPU_KERNEL_AUTO, 128},
+    {1, 4, 1, 0, &launch_small<4, false>, XSKNF_GPU_KERNEL_AUTO, 128},
+    {1, 4, 1, 0, &launch_small<4, true>, XSKNF_GPU_KERNEL_AUTO, 160},   // nt window loads
+    {1, 4, 1, 0, &launch_small<4, false, 1>, XSKNF_GPU_KERNEL_AUTO, 192},   // timing only: no parse / sum
+    {1, 4, 1, 0, &launch_small<4, false, 2>, XSKNF_GPU_KERNEL_AUTO, 224},   // timing only: no LDS either
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
     XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
