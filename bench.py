@@ -52,6 +52,7 @@ WORKLOADS = {
     # name: (length, layout, chunk, description)
     "1500": (1500, "aligned", 2048, "BASELINE config 3: 1500 B frames, aligned UMEM 2048 B chunks, data at +256"),
     "64": (64, "aligned", 2048, "BASELINE config 2: 64 B frames, aligned UMEM 2048 B chunks, data at +256"),
+    "570": (570, "aligned", 2048, "IMIX's middle size class alone: 570 B frames, aligned UMEM 2048 B chunks"),
     "imix": ("imix", "aligned", 2048, "IMIX 64/570/1500 B (7:4:1), 1M frames per GPU, aligned 2048 B chunks"),
     "jumbo": (9000, "unaligned", 0, "BASELINE config 5: 9000 B frames, unaligned-chunk UMEM, ~50% odd starts"),
     "config4": ("imix", "aligned", 2048,
@@ -492,14 +493,16 @@ def probes_for(res, reps=20):
 
 
 def traffic_for(name):
-    """HBM bytes of one step (every kernel of it) from the committed rocprofv3
-    PMC passes (tools/traffic.py -> profiles/traffic_<workload>.json), or None."""
+    """HBM bytes of one step (every kernel of every launch of it) from the
+    committed rocprofv3 PMC passes (tools/traffic.py ->
+    profiles/traffic_<workload>.json), or None."""
     p = os.path.join(ROOT, "profiles", f"traffic_{name}.json")
     if os.path.exists(p):
         try:
-            return json.load(open(p)).get("hbm_bytes_per_launch")
+            t = json.load(open(p))
         except (OSError, ValueError):
             return None
+        return t.get("hbm_bytes_per_step", t.get("hbm_bytes_per_launch"))
     return None
 
 
@@ -591,7 +594,8 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s checksummed",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "min_warmup_s": args.min_warmup_s,
-            "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(step_s * 1e3, 4), "kernel_steps": args.kernel_steps,
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u16 words summed in u32", "data": "synthetic",
             "mpps": round(mpps, 2),
             "config": {"workload": desc, "frames_per_gpu": prim["n"], "frame_len": length,

@@ -31,23 +31,30 @@ def main():
                          (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
     rows.sort()
     main_name = rows[0][1]
-    tail = 3 + 50 if kalone else 0
+    # a batch of more than 1M frames runs as 1M-frame launches (config 4 on one GPU)
+    per_step = -(-int(bench["config"]["frames_per_gpu"]) // (1 << 20))
+    ksteps = int(bench.get("kernel_steps", 50))
+    tail = per_step * (3 + ksteps) if kalone else 0
     mains = [r for r in rows if r[1] == main_name]
     step_main = mains[:len(mains) - tail] if tail else mains
     alone = mains[len(mains) - tail:] if tail else []
     scatter = [r for r in rows if "scatter_checks" in r[1]]
-    timed = step_main[-steps:]
+    timed = step_main[-steps * per_step:]
     out = {"bench_step_us": bench["roofline"]["step_us"],
            "bench_summing_alone_us": (bench["roofline"]["summing_kernel_alone"] or {}).get("us"),
-           "kernel": main_name,
+           "kernel": main_name, "launches_per_step": per_step,
            "step_kernel_us": {"mean": round(statistics.mean(r[2] for r in timed), 2),
                               "median": round(statistics.median(r[2] for r in timed), 2), "n": len(timed)}}
+    per_launch = statistics.mean(r[2] for r in timed)
     if scatter:
-        ts = scatter[-steps:]
+        ts = scatter[-steps * per_step:]
         out["scatter_checks_us"] = {"mean": round(statistics.mean(r[2] for r in ts), 2),
                                     "median": round(statistics.median(r[2] for r in ts), 2), "n": len(ts)}
+        per_launch += statistics.mean(r[2] for r in ts)
+    # the step from the trace: its launches' kernel durations (gaps between kernels excluded)
+    out["trace_step_us"] = round(per_step * per_launch, 2)
     if alone:
-        a = alone[3:]
+        a = alone[3 * per_step:]
         out["records_only_us"] = {"mean": round(statistics.mean(r[2] for r in a), 2),
                                   "median": round(statistics.median(r[2] for r in a), 2), "n": len(a)}
     print(json.dumps(out, indent=1))
