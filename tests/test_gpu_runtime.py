@@ -61,7 +61,7 @@ def test_gpu_hook_redirect_matches_oracle(frames, path, batch, two_phase):
 @pytest.mark.parametrize("depth", [2, 4])
 def test_gpu_hook_batches_in_flight(frames, path, depth):
     """Two-phase hook with up to `depth` batches out per worker (the context has
-    4 slots: a 5th submit completes the oldest itself)."""
+    5 slots: depth 4 plus the batch being submitted)."""
     cfg = R.make_config(["emu0"], batch_size=64)
     got, hs, st = run_loop(cfg, {0: frames}, two_phase=True, depth=depth, path=path, iterations=3)
     assert got[0] == [b for v, b in expected(frames, iterations=3) if v != -1]
