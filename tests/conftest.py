@@ -56,3 +56,69 @@ def _gpu_fault_attribution(request):
         torch.cuda.synchronize()
         time.sleep(0.02)
         torch.zeros(1, device="cuda").cpu()
+
+
+# ---- GPU memory-fault reporter (diagnostics for DESIGN 3's intermittent fault) ----
+#
+# HIP learns of a GPU memory fault from ROCr's system events and reports it as
+# hipErrorIllegalAddress at a later call, without the address.  ROCr hands the
+# event to every registered handler, so the test process registers one more
+# that prints the faulting virtual address and ROCr's reason mask (and appends
+# them to gpurun_out/memfault.log): a recurrence then says WHERE it faulted.
+_FAULT_HANDLER = None
+
+
+class _MemFault(__import__("ctypes").Structure):
+    import ctypes as _c
+    _fields_ = [("event_type", _c.c_uint32), ("pad", _c.c_uint32), ("agent", _c.c_uint64),
+                ("virtual_address", _c.c_uint64), ("fault_reason_mask", _c.c_uint32)]
+
+
+def _install_fault_reporter():
+    global _FAULT_HANDLER
+    import ctypes
+    if _FAULT_HANDLER is not None:
+        return
+    path = None
+    for line in open("/proc/self/maps"):
+        if "libhsa-runtime64" in line:
+            path = line.split()[-1]
+            break
+    if path is None:
+        return
+    try:
+        hsa = ctypes.CDLL(path, mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+        reg = hsa.hsa_amd_register_system_event_handler
+    except (OSError, AttributeError):
+        return
+    cb_t = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(_MemFault), ctypes.c_void_p)
+
+    def on_event(ev, _data):
+        e = ev.contents
+        if e.event_type == 0:   # HSA_AMD_GPU_MEMORY_FAULT_EVENT
+            msg = (f"GPU MEMORY FAULT: virtual address {e.virtual_address:#x}, reason mask "
+                   f"{e.fault_reason_mask:#x} (1 page not present, 2 read-only, 4 NX, 8 host-only, 0x20 imprecise)")
+            sys.stderr.write(msg + "\n")
+            sys.stderr.flush()
+            try:
+                os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+                with open(os.path.join(ROOT, "gpurun_out", "memfault.log"), "a") as f:
+                    f.write(msg + "\n")
+            except OSError:
+                pass
+        return 0
+
+    _FAULT_HANDLER = cb_t(on_event)
+    reg.argtypes = [cb_t, ctypes.c_void_p]
+    reg.restype = ctypes.c_int
+    reg(_FAULT_HANDLER, None)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_fault_reporter(request):
+    if request.node.get_closest_marker("gpu") is not None:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+            _install_fault_reporter()
+    yield

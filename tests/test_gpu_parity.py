@@ -6,6 +6,7 @@ Small seeded batches cover every branch of checksummer_user.c:30-112; the
 BASELINE configs run at full size (1M frames) against the threaded C oracle.
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -24,6 +25,12 @@ def _results(*tensors):
     a GPU memory fault asynchronously, from its event thread; with the 16
     oracle threads on every CPU of the box it surfaced only at the next HIP call
     after the oracle -- DESIGN 3, the round-2 fault)."""
+    import time
+    torch.cuda.synchronize()
+    # a second synchronize after a pause, with no new GPU work in between: a
+    # fault reported here came from work already done (the launch), one
+    # reported only at the copies below would implicate the copies
+    time.sleep(0.05)
     torch.cuda.synchronize()
     return tuple(t.cpu().numpy() for t in tensors)
 
@@ -511,6 +518,10 @@ def test_patch_list_overflow_writes_in_line(dev, shape):
     v = torch.empty(n, dtype=torch.int32, device=dev)
     opts = _lib.CsumOpts(1, O.REDIRECT, 1, 0)
     cfg = launch_cfg(shape, bpc=1)
+    # where the arrays lie (to place a faulting address)
+    print(f"overflow test arrays: umem [{umem.data_ptr():#x}, {umem.data_ptr() + umem.numel():#x}) "
+          f"descs [{descs.data_ptr():#x}, {descs.data_ptr() + 16 * n:#x}) v [{v.data_ptr():#x}, "
+          f"{v.data_ptr() + 4 * n:#x})", file=sys.stderr, flush=True)
     assert lib.xsknf_gpu_checksum_batch_cfg(
         ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), n, 0,
         ctypes.byref(opts), ctypes.c_void_p(v.data_ptr()), ctypes.byref(cfg), None) == 0
