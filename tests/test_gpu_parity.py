@@ -500,10 +500,11 @@ def test_concurrent_streams(dev):
                                    pytest.param((16, 3, 2, 0, 18, 1, 24),
                                                 marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only"))],
                          ids=_shape_id)
-def test_patch_list_overflow_writes_in_line(dev, shape):
-    """One block per CU: every wave gets more tiles than its LDS patch list
-    holds (6, 7 with the pool, 8 for the A/B 16 x 3 shape), so its later tiles
-    write their checks in-line; every verdict and byte still matches the
+def test_one_block_per_cu_asked_is_bit_exact(dev, shape):
+    """One block per CU asked for over 600K frames -- the launch of the three
+    unexplained faults, whose waves then had more tiles than their
+    LDS patch lists.  The launch now raises the grid until no wave does
+    (test_no_wave_passes_its_patch_list); every verdict and byte matches the
     oracle."""
     import ctypes
     from xsknf_amd import _lib
@@ -519,7 +520,7 @@ def test_patch_list_overflow_writes_in_line(dev, shape):
     opts = _lib.CsumOpts(1, O.REDIRECT, 1, 0)
     cfg = launch_cfg(shape, bpc=1)
     # where the arrays lie (to place a faulting address)
-    print(f"overflow test arrays: umem [{umem.data_ptr():#x}, {umem.data_ptr() + umem.numel():#x}) "
+    print(f"small-grid test arrays: umem [{umem.data_ptr():#x}, {umem.data_ptr() + umem.numel():#x}) "
           f"descs [{descs.data_ptr():#x}, {descs.data_ptr() + 16 * n:#x}) v [{v.data_ptr():#x}, "
           f"{v.data_ptr() + 4 * n:#x})", file=sys.stderr, flush=True)
     assert lib.xsknf_gpu_checksum_batch_cfg(
@@ -529,6 +530,33 @@ def test_patch_list_overflow_writes_in_line(dev, shape):
     _, ov = O.c_time_batch(host, hd, threads=16, reps=1)
     assert np.array_equal(gv, ov)
     assert np.array_equal(gu, host)
+
+
+TL_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "tl", "libxsknf_gpu.so")
+
+
+@pytest.mark.skipif(not os.path.exists(TL_LIB), reason="timeline build absent (make tl)")
+@pytest.mark.parametrize("frames_n,bpc", [(600_000, 1), (1 << 20, 1), (1 << 20, 8)])
+@pytest.mark.parametrize("window,limit", [(24, 6), (56, 7)], ids=["static", "pool"])
+def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
+    """launch_split sizes the grid so that no wave of a patch-list shape gets
+    more tiles than its list holds (static: each wave's share of the tiles;
+    pool: a wave with a full list claims no more), whatever blocks_per_cu asks
+    (DESIGN 3).  Per-wave tile counts from the timeline build (tools/timeline.py),
+    in a child process (the instrumented library is a second copy)."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, XSKNF_GPU_LIB=TL_LIB)
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "timeline.py"), "--workload", "imix",
+                          "--frames", str(frames_n), "--reps", "2", "--bpc", str(bpc),
+                          "--variant", f"16,2,2,0,18,1,{window}"],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    med = json.loads(out.stdout.strip().splitlines()[-1])["median"]
+    tiles = {int(k): v for k, v in med["tiles"].items()}
+    assert sum(k * v for k, v in tiles.items()) >= (frames_n + 63) // 64   # every tile (pool halves: more units)
+    assert max(tiles) <= limit, tiles
 
 
 @pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 0, 1, 52),

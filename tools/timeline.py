@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--rotate", type=int, default=1)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--variant", default="", help="lanes,chunks,u,ring,fused,kernel,window (default: product)")
+    ap.add_argument("--bpc", type=int, default=0, help="blocks per CU asked for (0: the shape's own)")
     a = ap.parse_args()
     length, layout = WL.get(a.workload, (int(a.workload) if a.workload.isdigit() else a.workload, "aligned"))
     dev = torch.device("cuda:0")
@@ -59,6 +60,8 @@ def main():
     if a.variant:
         v = [int(x) for x in a.variant.split(",")]
         cfg = _lib.LaunchCfg(v[0], v[1], v[2], 4, v[3], v[4], v[5], v[6])
+    if a.bpc:
+        cfg.blocks_per_cu = a.bpc
     verd = torch.empty(n, dtype=torch.int32, device=dev)
     tl = torch.zeros(8 * 65536, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
@@ -135,7 +138,7 @@ def main():
         })
     rows.sort(key=lambda x: x["kernel_us"])
     med = rows[len(rows) // 2]
-    print(json.dumps({"workload": a.workload, "cfg": [cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group,
+    print(json.dumps({"workload": a.workload, "frames": n, "blocks_per_cu": cfg.blocks_per_cu, "cfg": [cfg.lanes_per_frame, cfg.chunks_per_lane, cfg.frames_per_group,
                                                       cfg.lds_ring, cfg.fused_stores, cfg.kernel, cfg.window_chunks],
                       "median": med, "kernel_us_all": [r["kernel_us"] for r in rows]}))
 

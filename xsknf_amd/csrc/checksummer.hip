@@ -988,12 +988,13 @@ struct ItemStage {
 // header-window slots, dead after phase A when every check is deferred (the
 // only mode this variant runs in).  No stage registers: the kernel fits 4 waves
 // per SIMD at the 2-stage depth the register variant holds in 3.
+// (the s_nop: an SALU write of M0 needs one wait state before an LDS-DMA reads it)
 __device__ __forceinline__ void gload_lds_nt_asm(gchunk_ptr p, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(p), "s"(lds) : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(p), "s"(lds) : "memory", "m0");
 }
 
 __device__ __forceinline__ void gload_lds_asm(gchunk_ptr p, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(lds) : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(lds) : "memory", "m0");
 }
 
 template <int U, int NCH>
@@ -1139,11 +1140,13 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
 // sector, byte of the check in the sector, the check}.  The frame's final
 // verdict is stored in the tile's one verdict store, and the wave's patches
 // read neither records nor descriptors back: one round trip (the sectors)
-// instead of three.  A wave's tiles past its list (grids smaller than
-// residency, or a pool's faster waves) write their checks in-line.  (Parking
-// those as records in `verdicts` for the wave to patch after its list -- a
-// record path with three round trips -- raised an illegal-address fault twice
-// in full GPU suites, never alone or under the guard build: removed)
+// instead of three.  launch_split sizes the grid so that no wave has more
+// tiles than its list (the code for tiles past it -- checks in-line -- is kept
+// as a fallback).  Past the list, checks were first parked as records in
+// `verdicts` for the wave to patch after its list (three round trips), then
+// written in-line; launches past their lists faulted with an illegal address
+// three times in full GPU suites, twice with the records and once in-line,
+// never alone or under the guard build.
 #ifndef XSKNF_PATCH_TILES
 #define XSKNF_PATCH_TILES 6
 #endif
@@ -1158,6 +1161,14 @@ constexpr uint32_t kPatchValid = 1u << 23, kPatchWhole = 1u << 22, kPatchInWin =
 #endif
 constexpr bool kPatchLastSlot = XSKNF_PATCH_LAST_SLOT;   // the wave's last tile: sectors from its window slots
 constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with margin)
+
+// Tiles in a wave's patch list: 16 x 2 items fit 3 waves per SIMD (6 tiles per
+// wave at 1M frames; 7 with the pool, whose faster waves take more units), 16 x
+// 3 fit 2 (8 tiles per wave); the other shapes keep no list.
+template <int W, int NCH, int U, bool DMA, bool PFW, bool kPool>
+constexpr int patch_list_tiles() {
+  return (W == 8 && U >= 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
+}
 
 __device__ __forceinline__ uint2 patch_entry(const KernelArgs &a, const FrameRef &r, int u, uint16_t c, int wbytes) {
   const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
@@ -1277,12 +1288,10 @@ void checksum_kernel_split(const KernelArgs args) {
   __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kItemCap];
   __shared__ __attribute__((aligned(16))) uint4 meta[SW][kWave];
   __shared__ __attribute__((aligned(16))) uint32_t accb[SW][kWave];
-  // patch list tiles: 16 x 2 items fit 3 waves per SIMD (6 tiles per wave at 1M
-  // frames), 16 x 3 fit 2 (8 tiles per wave)
   constexpr bool kPool = SW > kWavesPerBlock;   // one block per CU: its waves share the CU's tiles
   // (jumbo keeps no list: with the pool and a 16-unit list, patching after the last unit tied the
   // scatter pass, 1463 vs 1461 us -- profiles/r02/ab_jumbo_tail.jsonl)
-  constexpr int PT = (W == 8 && U >= 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
+  constexpr int PT = patch_list_tiles<W, NCH, U, DMA, PFW, kPool>();
   __shared__ __attribute__((aligned(16))) uint2 plist[SW][PT > 0 ? PT * kWave : 1];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -1404,6 +1413,9 @@ void checksum_kernel_split(const KernelArgs args) {
     XSKNF_TL_START();
     if constexpr (kPool) {   // claim the next unit, and load its descriptors while this one streams
       uint32_t dq = 0;
+      // a wave whose patch list is full claims no more: launch_split sizes the
+      // grid so that the lists of a block's waves hold all of its units
+      if (list_ok && it + 1 >= PT) pool_live = false;
       if (pool_live && lane == 0) dq = __hip_atomic_fetch_add(&pool_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       tn = pool_live ? pool_unit(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dq), 0))) : kNoTile;
       pool_live = tn != kNoTile;
@@ -1805,7 +1817,7 @@ void checksum_kernel_small(const KernelArgs args) {
 // contiguous at slot + 16*g*LPF.
 
 __device__ __forceinline__ void dma16_nt(const void *gaddr, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt"
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
                :: "v"(gaddr), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
 }
 
@@ -2180,7 +2192,24 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
     }
     if (!fits) return launch_split<W, LPF, NCH, U, TL, DMA, PFW, kWavesPerBlock>(a, stream, blocks_per_cu);
   }
-  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave, SW)), dim3(SW * kWave), 0, stream, a);
+  uint32_t grid = grid_blocks(k, a.n, blocks_per_cu, kWave, SW);
+  constexpr uint32_t PT = patch_list_tiles<W, NCH, U, DMA, PFW, (SW > kWavesPerBlock)>();
+  if constexpr (PT > 0) {
+    // Enough blocks that every tile's check goes to a patch list, whatever
+    // blocks_per_cu asks or the device's CU count (blocks past residency start
+    // as others end): the static schedule deals each wave every waves-th tile,
+    // at most PT of them; a pool block's units (its tiles, the last SW of them
+    // halved) are at most SW x PT, and a wave with a full list claims no more.
+    // Waves past their lists wrote in-line in the launches of the three
+    // unexplained illegal-address faults of the GPU suites.
+    if (a.tail_scatter) {
+      const uint32_t tiles = (a.n + kWave - 1) / kWave;
+      constexpr uint32_t per_block = SW > kWavesPerBlock ? SW * (PT - 1) : SW * PT;
+      const uint32_t fit = (tiles + per_block - 1) / per_block;
+      if (grid < fit) grid = fit;
+    }
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(SW * kWave), 0, stream, a);
   return finish_launch(a, stream, "checksum_kernel_split launch");
 }
 
