@@ -59,6 +59,17 @@ WORKLOADS = {
                 "BASELINE config 4: 8,388,608 IMIX 64/570/1500 B frames (7:4:1) split into byte-balanced "
                 "contiguous shards, one per GPU, aligned 2048 B chunks"),
 }
+# The same batches with the UDP checksums a NIC's transmit offload fills in, as
+# the reference's own traffic carries them (tests/gen-traffic.lua:120,
+# bufs:offloadUdpChecksums()): the checksummer computes the value the frame
+# already holds for all but the frames whose single fold loses a carry
+# (checksummer_user.c:105-106), and the kernels leave those frames untouched.
+# The base workloads (checks 0 in every frame, so every check changes) are the
+# worst case and stay the headline.
+NIC = {"1500-nic": "1500", "imix-nic": "imix", "64-nic": "64", "jumbo-nic": "jumbo"}
+for _k, _b in NIC.items():
+    _l, _lay, _c, _d = WORKLOADS[_b]
+    WORKLOADS[_k] = (_l, _lay, _c, _d + "; UDP checksums as a NIC offload writes them (gen-traffic.lua:120)")
 
 
 def parse():
@@ -70,7 +81,7 @@ def parse():
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU (config4: global frames "
                    f"= {CONFIG4_FRAMES} unless --config4-frames)")
     p.add_argument("--config4-frames", type=int, default=CONFIG4_FRAMES)
-    p.add_argument("--secondary", default="64,imix,jumbo,config4",
+    p.add_argument("--secondary", default="64,imix,jumbo,config4,1500-nic,imix-nic,64-nic,jumbo-nic",
                    help="comma list of extra workloads timed after the primary ('' = none)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
@@ -203,9 +214,24 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     # step i processes batch i % K
     umem, descs, lens = frames.device_batch(n * K, np.tile(lens_in, K), layout=layout, chunk=chunk or frames.CHUNK,
                                             seed=seed, device=dev)
+    if name in NIC:
+        frames.offload_checks_device(umem, descs)
     # the caller knows its batch: longest frame and mean length (xsknf_gpu_checksum_batch_lens)
     hint, mean = int(lens.max()), int(lens_in.mean())
     cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=hint, frame_len_mean=mean)
+    # A frame that already holds the check the kernel computes is left untouched
+    # (include/xsknf_gpu.h), so a pass over a batch the previous pass just
+    # checksummed would write nothing.  Every step must see the frames as they
+    # arrive (inputs reset between repeats):
+    # * base workloads (checks 0, every one changes): each visit of a batch
+    #   alternates csum_iterations 1 and 2, so every check the previous visit
+    #   wrote changes again -- the step's work is that of fresh frames (the
+    #   kernel's cost does not depend on the iteration count: closed form);
+    # * NIC workloads: the checks the first pass changed (the carry-loss frames)
+    #   are put back between steps, outside the step's own HIP events.
+    cs_alt = Checksummer(ChecksummerOptions(csum_iterations=2), num_interfaces=1, frame_len_hint=hint,
+                         frame_len_mean=mean)
+    nic = name in NIC
     verdicts = torch.empty(n * K, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     umem_ptr, umem_size = umem.data_ptr(), umem.numel()
@@ -222,12 +248,32 @@ def time_workload(name, args, world, rank, dev, seed, primary):
         hi = int((offs + dk["len"]).max())
         sample = (umem[:hi].cpu().numpy(), dk, k)
 
+    restore = None
+    if nic:
+        # the check bytes of every frame as the NIC wrote them; after one pass,
+        # keep only those the pass changed
+        addr = descs[:, 0]
+        starts = (addr & ((1 << 48) - 1)) + ((addr >> 48) & 0xFFFF)
+        at = torch.stack([starts + 40, starts + 41], 1).reshape(-1).clamp_(max=umem_size - 1)
+        orig = umem[at]
+        for j in range(K):
+            cs.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[j], n, v_ptrs[j], 0, stream.cuda_stream)
+        changed = umem[at] != orig
+        restore = (at[changed], orig[changed])
+        umem[restore[0]] = restore[1]
+        del addr, starts, at, orig, changed
+        torch.cuda.synchronize()
+
     it = [0]
 
     def step():
         j = it[0] % K
+        c = cs_alt if (not nic and (it[0] // K) & 1) else cs
         it[0] += 1
-        cs.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[j], n, v_ptrs[j], 0, stream.cuda_stream)
+        c.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[j], n, v_ptrs[j], 0, stream.cuda_stream)
+
+    def put_back():
+        umem[restore[0]] = restore[1]
 
     # W untimed warmup steps, continued until at least --min-warmup-s of
     # warmup has run: measured on MI355X, 10 steps (3 ms) leave the step ~3 %
@@ -235,27 +281,44 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     t_w = time.perf_counter()
     for _ in range(args.warmup):
         step()
+        if nic:
+            put_back()
     torch.cuda.synchronize()
     while time.perf_counter() - t_w < args.min_warmup_s:
         for _ in range(10):
             step()
+            if nic:
+                put_back()
         torch.cuda.synchronize()
     barrier(world)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     first = it[0]
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
+    if nic:   # each step on the frames as they arrived, timed by its own events
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        for e0, e1 in evs:
+            e0.record(stream)
+            step()
+            e1.record(stream)
+            put_back()
+    else:
+        ev0.record(stream)
+        for _ in range(args.steps):
+            step()
+        ev1.record(stream)
     barrier(world)
     wall = time.perf_counter() - t0
     # frame bytes of the timed steps (the K batches differ slightly in length mix)
     bytes_len = sum(batch_bytes[i % K] for i in range(first, first + args.steps)) // args.steps
-    step_ms = ev0.elapsed_time(ev1) / args.steps        # HIP events on the launch stream
+    step_ms = (sum(e0.elapsed_time(e1) for e0, e1 in evs) if nic else ev0.elapsed_time(ev1)) / args.steps
     wall_max = allreduce_max(wall, world)
     step_ms_max = allreduce_max(step_ms, world)
+    if not nic:
+        # leave batch 0 as one -i 1 pass leaves it (the CPU leg checks it)
+        cs.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[0], n, v_ptrs[0], 0, stream.cuda_stream)
+        torch.cuda.synchronize()
 
     # the summing kernel alone, for reference beside the step: records-only
     # mode (include/xsknf_gpu.h fused_stores = 3), same shape, same stream, HIP
@@ -346,16 +409,19 @@ def root_scatter_leg(args, world, rank, dev):
     if cdev == "cpu":
         lu, ld = lu.to(dev), ld.to(dev)
     n_local = ld.shape[0]
-    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=1500)
+    # alternating csum_iterations 1 / 2: every pass changes every check (a pass
+    # over frames the previous pass left would write nothing, time_workload)
+    css = [Checksummer(ChecksummerOptions(csum_iterations=i), num_interfaces=1, frame_len_hint=1500)
+           for i in (1, 2)]
     stream = torch.cuda.current_stream(dev)
-    for _ in range(3):
-        v = cs.process_batch(lu, ld)
+    for i in range(3):
+        v = css[i & 1].process_batch(lu, ld)
     barrier(world)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     reps = 10
-    for _ in range(reps):
-        v = cs.process_batch(lu, ld)
+    for i in range(reps):
+        v = css[(i + 1) & 1].process_batch(lu, ld)
     e1.record(stream)
     barrier(world)
     step_s = allreduce_max(e0.elapsed_time(e1) / reps / 1e3, world)
@@ -537,7 +603,7 @@ def main():
     for name in [s for s in args.secondary.split(",") if s and s != args.workload]:
         r = time_workload(name, args, world, rank, dev, seed, primary=False)
         r["world"] = world
-        if world == 1 and not args.no_probes:
+        if world == 1 and not args.no_probes and name not in NIC:   # same bytes as the base workload
             r["probes"] = probes_for(r)
         sec[name] = step_summary(r, args.steps)
         del r

@@ -119,6 +119,12 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * its own tiles after its last one, instead of a second launch (the default
  * with 2 up to 4 KiB frames: every check deferred, then patched in bursts at
  * the waves' ends).
+ * A frame whose computed check equals the check it already holds (traffic whose
+ * UDP checksums a NIC filled in, tests/gen-traffic.lua:120) ends with the bytes
+ * it began with (:68 clears the check, :108 stores the same value), so the
+ * product kernels write nothing for it and leave its verdict (no record in mode
+ * 3).  Adding 32 to `fused_stores` writes such checks anyway (A/B only; the
+ * UMEM and verdicts come out the same).
  * `kernel` = XSKNF_GPU_KERNEL_SPLIT selects the split kernel (the default for
  * every hint): lane l of a wave parses, sums and finishes frame l of a
  * 64-frame tile from its first `window_chunks` & 15 (4..7, or 8) chunks, and the

@@ -338,6 +338,112 @@ def test_every_launch_shape_is_bit_exact(dev, shape, layout):
     assert np.array_equal(umem.cpu().numpy(), ou)
 
 
+def _nic_batch(seed, layout, n=2500):
+    """Mixed lengths with the UDP checksums a NIC offload writes
+    (tests/gen-traffic.lua:120), then 5 % edge cases."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 3000, size=n).astype(np.uint32)
+    if layout == "aligned":
+        b = frames.aligned_batch(n, np.minimum(lens, 1792), chunk=2048, seed=seed)
+    else:
+        b = frames.unaligned_batch(n, lens, seed=seed)
+    frames.offload_checks_host(b)
+    frames.inject_edge_cases(b, 0.05, seed=seed + 1)
+    return b
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[_shape_id(s) for s in SHAPES])
+@pytest.mark.parametrize("store_unchanged", [False, True], ids=["elide", "store32"])
+def test_nic_offloaded_checks_every_shape(dev, shape, store_unchanged):
+    """Frames whose UDP checksums a NIC already filled in: the checksummer
+    computes the value each frame holds for all but its carry-loss frames, and
+    every shape leaves those frames untouched (or rewrites the same bytes with
+    fused_stores + 32): every verdict and byte equal to the oracle's."""
+    import ctypes
+    from xsknf_amd import _lib
+    lib = _lib.load()
+    b = _nic_batch(sum(shape) + 7, "unaligned" if sum(shape) & 1 else "aligned")
+    ou, ov = run_oracle(b, iters=1, action=O.REDIRECT, nif=3, ingress=1)
+    umem = torch.from_numpy(b.umem).to(dev)
+    descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+    v = torch.empty(b.n, dtype=torch.int32, device=dev)
+    cfg = launch_cfg(shape)
+    if store_unchanged:
+        cfg.fused_stores += 32
+    rc = lib.xsknf_gpu_checksum_batch_cfg(
+        ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), b.n, 1,
+        ctypes.byref(_lib.CsumOpts(1, O.REDIRECT, 3, 0)), ctypes.c_void_p(v.data_ptr()),
+        ctypes.byref(cfg), None)
+    assert rc == 0
+    gv, gu = _results(v, umem)
+    assert np.array_equal(gv, ov)
+    assert np.array_equal(gu, ou)
+
+
+@pytest.mark.parametrize("shape", [(1, 5, 2, 0), (32, 3, 2, 0), (16, 2, 2, 0, 0, 1, 24), (16, 2, 2, 0, 0, 1, 56),
+                                   (16, 3, 2, 0, 0, 1, 52)],
+                         ids=["lane", "reg32", "split-w8", "split-pool", "split-w4-pool"])
+def test_records_mark_exactly_the_changed_checks(dev, shape):
+    """Records-only mode over NIC-checksummed frames: a frame gets a record
+    exactly when the oracle changes its check bytes (the carry-loss frames,
+    the edge cases with odd headers); every other frame carries its verdict.
+    So the kernels elide exactly the writes that would not change a byte."""
+    import ctypes
+    from xsknf_amd import _lib
+    lib = _lib.load()
+    b = _nic_batch(91, "unaligned", n=20000)
+    ou, ov = run_oracle(b, iters=1, action=O.REDIRECT, nif=1)
+    offs = b.frame_offsets().astype(np.int64)
+    lens = b.descs["len"].astype(np.int64)
+    umem = torch.from_numpy(b.umem).to(dev)
+    descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+    v = torch.empty(b.n, dtype=torch.int32, device=dev)
+    cfg = launch_cfg(shape, fused=3)
+    assert lib.xsknf_gpu_checksum_batch_cfg(
+        ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), b.n, 0,
+        ctypes.byref(_lib.CsumOpts(1, O.REDIRECT, 1, 0)), ctypes.c_void_p(v.data_ptr()),
+        ctypes.byref(cfg), None) == 0
+    gv, gu = _results(v, umem)
+    assert np.array_equal(gu, b.umem)
+    rec = gv.view(np.uint32)
+    tagged = (rec & 0xC0000000) == 0x40000000
+    changed = np.zeros(b.n, bool)
+    for i in np.flatnonzero(ov >= 0):          # summed frames: their check is at u + 6
+        u = 14 + 4 * (int(b.umem[offs[i] + 14]) & 0x0F)
+        at = int(offs[i]) + u + 6
+        if at + 2 <= offs[i] + lens[i]:
+            changed[i] = not np.array_equal(ou[at:at + 2], b.umem[at:at + 2])
+    assert np.array_equal(tagged, changed)
+    assert 0 < tagged.sum() < 0.1 * b.n
+    assert np.array_equal(np.where(tagged, 0, gv), np.where(tagged, 0, ov))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("length,layout", [(1500, "aligned"), ("imix", "aligned"), (64, "aligned"),
+                                           (9000, "unaligned")])
+def test_full_size_nic_offloaded_bit_exact(dev, length, layout):
+    """The bench's NIC-checksum workloads at full size (1M frames, 1 % edge
+    cases): bit-exact with the oracle; the oracle changes the checks of < 5 %
+    of the frames (carry losses and edge cases), the rest stay as they were."""
+    n = 1 << 20
+    umem, descs, lens = frames.device_batch(n, length, layout=layout, device=dev, seed=123)
+    frames.offload_checks_device(umem, descs)
+    host_in = umem.cpu().numpy()
+    hd = descs.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1).copy()
+    frames.inject_edge_cases(frames.HostBatch(host_in, hd, layout), 0.01, seed=124)
+    umem.copy_(torch.from_numpy(host_in))
+    descs.copy_(torch.from_numpy(hd.view(np.int64).reshape(n, 2)))
+    before = host_in.copy()
+    v = Checksummer(frame_len_hint=int(lens.max()), frame_len_mean=int(lens.mean())).process_batch(umem, descs)
+    gv, gu = _results(v, umem)
+    _, ov = O.c_time_batch(host_in, hd, threads=16, reps=1)
+    assert np.array_equal(gv, ov)
+    assert np.array_equal(gu, host_in)
+    offs = frames.HostBatch(before, hd, layout).frame_offsets().astype(np.int64)
+    at = offs[(hd["len"] >= 42)] + 40
+    assert (gu[at] != before[at]).mean() < 0.05
+
+
 @pytest.mark.parametrize("shape", [(32, 3, 2, 0), (64, 2, 4, 0), (16, 3, 1, 0, 0, 1, 24), (16, 2, 2, 0, 0, 1, 20),
                                    (16, 2, 2, 0, 0, 1, 56), (16, 3, 2, 0, 0, 1, 52)],
                          ids=["reg32", "reg64", "split-w8", "split-w4", "split-pool", "split-w4-pool"])

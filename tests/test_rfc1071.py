@@ -53,3 +53,41 @@ def test_receive_check_catches_a_wrong_check():
     b.umem[offs[17] + 40] ^= 0x10
     idx, V = _verify(b)
     assert V[list(idx).index(17)] not in (0xFFFF, 0x0001)
+
+
+@pytest.mark.parametrize("length,layout", [(1500, "aligned"), ("imix", "aligned"), (64, "aligned"),
+                                           (9000, "unaligned"), ("imix", "unaligned")])
+def test_nic_offloaded_checks_verify_and_mostly_stay(length, layout):
+    """frames.offload_checks_host gives each frame the check a NIC's UDP
+    offload writes (tests/gen-traffic.lua:120): every frame verifies as 0xFFFF,
+    and the oracle, run over them, changes only the checks of its carry-loss
+    frames (the RFC value + 1) -- no other byte."""
+    b = (frames.aligned_batch(6000, length, seed=5) if layout == "aligned"
+         else frames.unaligned_batch(6000, length, seed=5))
+    assert frames.offload_checks_host(b) == b.n
+    idx, V = _verify(b)
+    assert idx.size == b.n and np.all(V == 0xFFFF)
+    before = b.umem.copy()
+    O.c_process_batch(b.umem, b.descs)
+    offs = b.frame_offsets().astype(np.int64)
+    diff = np.flatnonzero(before != b.umem)
+    assert np.isin(diff, np.concatenate([offs + 40, offs + 41])).all()
+    changed = np.unique(np.searchsorted(np.sort(offs), diff, side="right"))
+    assert changed.size < {64: 0.001, 1500: 0.01, 9000: 0.05}.get(length, 0.01) * b.n + 1
+    idx2, V2 = _verify(b)
+    assert np.all((V2 == 0xFFFF) | (V2 == 0x0001))
+
+
+def test_offload_skips_malformed_frames():
+    """Edge-case frames (non-IPv4, non-UDP, ihl != 5, short) keep their bytes."""
+    b = frames.unaligned_batch(3000, "imix", seed=8)
+    frames.inject_edge_cases(b, 0.3, seed=9)
+    before = b.umem.copy()
+    frames.offload_checks_host(b)
+    offs = b.frame_offsets().astype(np.int64)
+    lens = b.descs["len"].astype(np.int64)
+    ok = np.array([lens[i] >= 42 and before[offs[i] + 12] == 8 and before[offs[i] + 13] == 0
+                   and before[offs[i] + 14] == 0x45 and before[offs[i] + 23] == 17 for i in range(b.n)])
+    diff = np.flatnonzero(before != b.umem)
+    allowed = np.concatenate([offs[ok] + 40, offs[ok] + 41])
+    assert np.isin(diff, allowed).all()

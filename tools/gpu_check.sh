@@ -10,7 +10,7 @@ cd "$R"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > "$OUT/gpu_tests.log" 2>&1 || { echo "gpu tests failed"; tail -30 "$OUT/gpu_tests.log"; exit 1; }
 tail -3 "$OUT/gpu_tests.log"
-timeout -k 10 240 python bench.py --secondary 64,config4,imix,jumbo > "$OUT/bench_all.json" 2> "$OUT/bench_all.err" \
+timeout -k 10 400 python bench.py > "$OUT/bench_all.json" 2> "$OUT/bench_all.err" \
     || { echo "bench failed"; tail -30 "$OUT/bench_all.err"; exit 1; }
 cat "$OUT/bench_all.json"
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \

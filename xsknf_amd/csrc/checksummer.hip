@@ -342,6 +342,15 @@ __device__ __forceinline__ uint16_t check_of(const Header &h, uint32_t P, uint32
   return static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));
 }
 
+// Whether the new check c must be written.  :68 clears the check and :108
+// stores c: when c is the value the frame already holds (a NIC filled in the
+// UDP checksum, tests/gen-traffic.lua:120 -- the reference's own traffic), the
+// frame ends with the bytes it began with, and neither its sector nor a record
+// is written.  (old_check is the same 2 bytes read as a little-endian u16.)
+__device__ __forceinline__ bool check_changes(const KernelArgs &a, const Header &h, uint16_t c) {
+  return c != static_cast<uint16_t>(h.old_check) || a.store_unchanged;
+}
+
 // The word this frame leaves in verdicts[f] after the summing pass; the check
 // bytes are written here only in single-pass (fused) mode.
 __device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const FrameRef &r, const Header &h,
@@ -349,6 +358,7 @@ __device__ __forceinline__ int32_t frame_result(const KernelArgs &a, const Frame
                                                 bool sector_done = false) {
   if (!do_sum) return verdict;
   const uint16_t c = check_of(h, P, a.payload_mult);
+  if (!check_changes(a, h, c)) return verdict;
   if (static_cast<uint32_t>(r.len) >= a.defer_min_len)
     return static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
   if (!sector_done) *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
@@ -440,7 +450,11 @@ __device__ __forceinline__ void finish_long_frames(const KernelArgs &a, uint32_t
       const uint32_t sum = lds_i32(part + 4 * i) + a.payload_mult * Prest;   // :92-103
       const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((sum & 0xffffu) + (sum >> 16)));
       int32_t res = a.fwd_verdict;
-      if (static_cast<uint32_t>(r.len) >= a.defer_min_len)
+      // the old check, for check_changes (pass 0's window is gone: 2 bytes from the frame)
+      const uint16_t old = static_cast<uint16_t>(r.fp[u + 6] | (r.fp[u + 7] << 8));
+      if (c == old && !a.store_unchanged) {
+        // the frame already holds c: nothing to write
+      } else if (static_cast<uint32_t>(r.len) >= a.defer_min_len)
         res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(u) << 16) | c);
       else *reinterpret_cast<uint16_t *>(r.fp + u + 6) = c;   // :108
       lds_store_i32(rec + 4 * i, res);
@@ -559,8 +573,10 @@ __device__ __forceinline__ int32_t process_regs(const KernelArgs &args, const Fr
   if (args.sector_stores && __builtin_amdgcn_ballot_w64(do_sum && r.nch <= LPF * NCH &&
                                                         static_cast<uint32_t>(r.len) < args.defer_min_len)) {
     const uint32_t P = group_bcast_last<LPF>(P0, lane_id());
-    if (do_sum && r.nch <= LPF * NCH && static_cast<uint32_t>(r.len) < args.defer_min_len)
-      sector_done = store_check_sector<LPF, NCH>(r, h, check_of(h, P, args.payload_mult), v, gl);
+    const uint16_t c = check_of(h, P, args.payload_mult);
+    if (do_sum && r.nch <= LPF * NCH && static_cast<uint32_t>(r.len) < args.defer_min_len &&
+        check_changes(args, h, c))
+      sector_done = store_check_sector<LPF, NCH>(r, h, c, v, gl);
   }
   return (gl == LPF - 1 && r.exists)
              ? step_result(args, r, h, verdict, do_sum, P0, LPF * NCH, part_addr, sector_done) : 0;
@@ -697,6 +713,7 @@ __device__ __forceinline__ LaneOut process_lane(const KernelArgs &args, const Fr
   for (int k = 0; k < NCH; ++k) chunk_sum(v[k], 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
   for (int k = NCH; k < r.nch; ++k) chunk_sum(*XSKNF_GLD(r.cp + k, 16), 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
   const uint16_t c = check_of(h, acc_lo + (acc_hi << 8), args.payload_mult);
+  if (!check_changes(args, h, c)) return out;
   if (static_cast<uint32_t>(r.len) >= args.defer_min_len) {
     out.res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
     return out;
@@ -1504,7 +1521,7 @@ void checksum_kernel_split(const KernelArgs args) {
     int32_t res = r.exists ? verdict : 0;
     LaneOut o = {res, false, slot, r.fp};
     uint2 ent = make_uint2(0, 0);
-    if (do_sum && !more) {
+    if (do_sum && !more && check_changes(args, h, check_of(h, PA, args.payload_mult))) {
       const uint16_t c = check_of(h, PA, args.payload_mult);
       if (static_cast<uint32_t>(r.len) >= defer_min) {
         if (to_list) ent = patch_entry(args, r, h.u, c, 16 * W);
@@ -1593,9 +1610,9 @@ void checksum_kernel_split(const KernelArgs args) {
       // is written as that whole sector: patched in the lane's slot (the window
       // is still there) and stored by the wave, as in phase A
       LaneOut oc = {0, false, slot, r.fp};
-      if (more) {
-        const uint32_t s = part + args.payload_mult * lds_i32(ab + 4 * lane);   // :92-103
-        const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));
+      const uint32_t s = part + args.payload_mult * lds_i32(ab + 4 * lane);   // :92-103
+      const uint16_t c = static_cast<uint16_t>(~static_cast<uint16_t>((s & 0xffffu) + (s >> 16)));
+      if (more && check_changes(args, h, c)) {
         const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
         const uintptr_t ck = f0 + h.u + 6;
         const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
@@ -2396,6 +2413,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
   a.sector_stores = 1;
   a.plain_sector = 0;
   a.tail_scatter = 0;
+  a.store_unchanged = 0;
   a.seq = 0;
   a.count_records = 0;
   // aligned-down descriptor address: inside the descriptor array's own page
@@ -2407,8 +2425,9 @@ constexpr uint32_t kLaunchFrames = 1u << 20;
 
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
-  const int mode = cfg.fused_stores & 3;          // + 4: 2-byte in-line stores, + 8: plain sector stores
-  if (cfg.fused_stores < 0 || cfg.fused_stores > 31) return -EINVAL;
+  // + 4: 2-byte in-line stores, + 8: plain sector stores, + 32: write unchanged checks too
+  const int mode = cfg.fused_stores & 3;
+  if (cfg.fused_stores < 0 || cfg.fused_stores > 63) return -EINVAL;
   const Variant *v = find_variant(cfg);
   if (!v) return -EINVAL;
   KernelArgs a = base;
@@ -2416,6 +2435,7 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (mode == 3) a.no_scatter = 1;   // records only: the caller applies the checks
   if (cfg.fused_stores & 4) a.sector_stores = 0;
   if (cfg.fused_stores & 8) a.plain_sector = 1;
+  if (cfg.fused_stores & 32) a.store_unchanged = 1;
   // + 16: the split kernel patches its deferred checks itself (no scatter launch)
   a.tail_scatter = (cfg.fused_stores & 16) && v->kernel == XSKNF_GPU_KERNEL_SPLIT && a.defer_min_len != kNoDefer &&
                    !a.no_scatter;

@@ -31,6 +31,8 @@ struct KernelArgs {
                            // 0: non-temporal
   uint32_t tail_scatter;   // 1 (split kernel): each wave patches the deferred checks of its
                            // own tiles after its last tile; no scatter launch
+  uint32_t store_unchanged;  // 1: write a check even when the frame already holds it
+                             // (A/B); 0: such a frame is left untouched
 };
 
 // Check record parked in verdicts[f] by the summing pass (deferred stores):

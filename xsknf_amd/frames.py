@@ -179,6 +179,73 @@ def inject_edge_cases(b: HostBatch, frac: float, *, seed: int = SEED + 1) -> np.
     return np.sort(sel)
 
 
+# ---- NIC checksum offload ------------------------------------------------
+
+def _offload(umem, starts, lens, budget: int = 1 << 24) -> int:
+    """UDP checksums as a NIC's transmit offload fills them in (RFC 768: the
+    one's-complement sum, fully folded, of the pseudo-header {src, dst, 17,
+    udp.len} and the UDP bytes with the check as 0; a result of 0 is sent as
+    0xFFFF), written big-endian at frame offset 40.  Only well-formed frames
+    are touched: Ethernet/IPv4, ihl 5, protocol 17, len >= 42.  `umem` is a
+    uint8 torch tensor (any device), `starts` / `lens` int64 tensors on the same
+    device.  Returns the number of frames given a check."""
+    import torch
+
+    dev = umem.device
+    n = int(starts.shape[0])
+    done = 0
+    if n == 0:
+        return 0
+    maxlen = int(lens.max())
+    step = max(256, budget // max(64, maxlen))
+    for a in range(0, n, step):
+        st, ln = starts[a:a + step], lens[a:a + step]
+        width = max(42, int(ln.max()))
+        col = torch.arange(width, device=dev)
+        idx = (st[:, None] + col[None, :]).clamp_(max=umem.numel() - 1)
+        f = umem[idx].to(torch.int64)
+        f = torch.where(col[None, :] < ln[:, None], f, torch.zeros_like(f))
+        ok = ((ln >= 42) & (f[:, 12] == 0x08) & (f[:, 13] == 0x00) & (f[:, 14] == 0x45) & (f[:, 23] == 17))
+        be = lambda i: (f[:, i] << 8) | f[:, i + 1]   # noqa: E731
+        s = be(26) + be(28) + be(30) + be(32) + 17 + be(38)
+        udp = f[:, 34:].clone()
+        udp[:, 6:8] = 0                               # the check itself counts as 0
+        s = s + (udp[:, 0::2].sum(dim=1) << 8) + udp[:, 1::2].sum(dim=1)
+        for _ in range(4):
+            s = (s & 0xFFFF) + (s >> 16)
+        c = (~s) & 0xFFFF
+        c = torch.where(c == 0, torch.full_like(c, 0xFFFF), c)
+        sel = ok.nonzero().squeeze(1)
+        if sel.numel():
+            at = st[sel] + 40
+            umem[at] = (c[sel] >> 8).to(torch.uint8)
+            umem[at + 1] = (c[sel] & 0xFF).to(torch.uint8)
+        done += int(sel.numel())
+    return done
+
+
+def offload_checks_host(b: HostBatch) -> int:
+    """Give a host batch's well-formed frames the UDP checksums a NIC's offload
+    computes (the reference's traffic: tests/gen-traffic.lua:120,
+    `bufs:offloadUdpChecksums()`), in place.  Apply before inject_edge_cases."""
+    import torch
+
+    return _offload(torch.from_numpy(b.umem), torch.from_numpy(b.frame_offsets().astype(np.int64)),
+                    torch.from_numpy(b.descs["len"].astype(np.int64)))
+
+
+def offload_checks_device(umem, descs) -> int:
+    """offload_checks_host for a device batch (umem uint8, descs int64 (n, 2)
+    holding struct xdp_desc, as device_batch returns them)."""
+    import torch
+
+    addr = descs[:, 0]
+    mask = (1 << OFFSET_SHIFT) - 1
+    starts = (addr & mask) + ((addr >> OFFSET_SHIFT) & 0xFFFF)
+    lens = descs[:, 1] & 0xFFFFFFFF
+    return _offload(umem, starts.to(torch.int64), lens.to(torch.int64))
+
+
 # ---- device builders (torch) ---------------------------------------------
 
 def device_batch(n: int, length, *, layout: str = "aligned", chunk: int = CHUNK,
