@@ -10,6 +10,14 @@ kernel 1 = the split kernel with a `window`-chunk header window per lane).
 
 Every variant's output (verdicts + whole UMEM) is compared with the default
 shape's output, so a tuning run is also a cross-variant parity check.
+
+--checks zero (default): the frames' checks are 0, so every check changes; the
+timed launches alternate csum_iterations 1 and 2 per visit of a batch, so each
+launch rewrites every check (a launch over frames the previous one left would
+write nothing: the kernels skip checks a frame already holds).  --checks nic:
+the checks a NIC's UDP offload writes (frames.offload_checks_device), all but
+the carry-loss frames already right; the launches all use -i 1 (after the first
+pass the carry-loss frames hold their value too: the same for every variant).
 """
 import argparse
 import ctypes
@@ -40,6 +48,7 @@ def main():
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--checks", default="zero", choices=["zero", "nic"])
     ap.add_argument("--rotate", type=int, default=1,
                     help="batches the timed launches cycle through (bench.py's rotation: keeps a small-frame "
                          "batch out of the Infinity Cache between launches)")
@@ -50,10 +59,13 @@ def main():
     base_lens = frames._lens(a.frames, length, __import__("numpy").random.default_rng(frames.SEED))
     umem0, descs_all, lens_all = frames.device_batch(a.frames * K, __import__("numpy").tile(base_lens, K),
                                                      layout=layout, device=dev)
+    if a.checks == "nic":
+        frames.offload_checks_device(umem0, descs_all)
     descs = descs_all[:a.frames]
     lens = lens_all[:a.frames]
     lib = _lib.load()
     opts = _lib.CsumOpts(1, 0, 1, 0)
+    opts2 = _lib.CsumOpts(2, 0, 1, 0)
     n = a.frames
     hint = int(lens.max())
     dflt = _lib.LaunchCfg()
@@ -73,11 +85,11 @@ def main():
 
     rot = [0]
 
-    def run(cfg, um, vv, j=0):
+    def run(cfg, um, vv, j=0, alt=False):
         c = _lib.LaunchCfg(cfg[0][0], cfg[0][1], cfg[0][2], cfg[1], cfg[0][3], cfg[0][4], cfg[0][5], cfg[0][6])
         rc = lib.xsknf_gpu_checksum_batch_cfg(ctypes.c_void_p(um.data_ptr()), um.numel(),
                                               ctypes.c_void_p(descs_all.data_ptr() + 16 * n * j), n, 0,
-                                              ctypes.byref(opts), ctypes.c_void_p(vv.data_ptr()),
+                                              ctypes.byref(opts2 if alt else opts), ctypes.c_void_p(vv.data_ptr()),
                                               ctypes.byref(c), ctypes.c_void_p(stream.cuda_stream))
         _lib.check(rc, f"cfg {cfg}")
 
@@ -97,13 +109,15 @@ def main():
         del u, v
     for r in range(a.rounds):
         for c in cfgs:
+            def visit():
+                rot[0] += 1
+                run(c, umem, verd, rot[0] % K, a.checks == "zero" and bool((rot[0] // K) & 1))
             for _ in range(2):
-                run(c, umem, verd)
+                visit()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(a.reps):
-                rot[0] += 1
-                run(c, umem, verd, rot[0] % K)
+                visit()
             e1.record(stream)
             torch.cuda.synchronize()
             times[c].append(e0.elapsed_time(e1) / a.reps * 1e3)
@@ -111,7 +125,7 @@ def main():
     alg = blen + n * 22
     for c in cfgs:
         med = statistics.median(times[c])
-        print(json.dumps({"workload": a.workload, "shape": c[0], "bpc": c[1], "us": round(med, 2),
+        print(json.dumps({"workload": a.workload, "checks": a.checks, "shape": c[0], "bpc": c[1], "us": round(med, 2),
                           "min_us": round(min(times[c]), 2),
                           "gbs_checksummed": round(blen / med / 1e3, 1),
                           "roofline_frac": round(alg / med / 1e3 / 8000, 4),

@@ -1793,7 +1793,9 @@ void checksum_kernel_small(const KernelArgs args) {
       const uintptr_t ck = f0 + h.u + 6;
       const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
       const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
-      if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
+      if (!check_changes(args, h, c)) {
+        // the frame already holds c
+      } else if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
           sec + 64 <= c0 + 16 * kWin) {
         const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
         lds_store_u8(at, static_cast<uint8_t>(c));
