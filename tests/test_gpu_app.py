@@ -71,7 +71,10 @@ def gpu():
      False),
     # the one-call hook (one batch at a time) instead of the default two-phase one
     (["-i", "emu0"], ["-q", "-s", "-c", "DROP", "-G", "20000:64"], 20000, 1, False),
-], ids=["drop-64", "redirect-570-depth4", "redirect-1500-w2", "staged-570", "drop-64-gpu-sync"])
+    # the resident kernel's ring (no launch per batch), two workers, REDIRECT, four batches out
+    (["-i", "emu0", "-w", "2", "-b", "64"], ["-q", "-d", "4", "-c", "REDIRECT", "-g", "RESIDENT", "-G", "12000:570"],
+     12000, 2, True),
+], ids=["drop-64", "redirect-570-depth4", "redirect-1500-w2", "staged-570", "drop-64-gpu-sync", "resident-570-w2"])
 def test_stats_txt_on_sigusr1(gpu, clean_ctx, tmp_path, lib_args, app_args, count, queues, tx):
     want = count * queues
     with clean_ctx.Pool(1) as pool:

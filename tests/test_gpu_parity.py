@@ -482,7 +482,7 @@ def test_records_only_mode(dev, shape):
 
 
 @pytest.mark.parametrize("order", ["rx", "scattered"])
-@pytest.mark.parametrize("path", ["zerocopy", "staged"])
+@pytest.mark.parametrize("path", ["zerocopy", "staged", "resident"])
 @pytest.mark.parametrize("layout", ["aligned", "unaligned"])
 def test_host_path_bit_exact(dev, path, layout, order):
     """UMEM in (pinned) host memory, descriptors / verdicts in host arrays.
@@ -511,7 +511,7 @@ def test_host_path_bit_exact(dev, path, layout, order):
     assert np.array_equal(umem, ou)
 
 
-@pytest.mark.parametrize("path", ["zerocopy", "staged"])
+@pytest.mark.parametrize("path", ["zerocopy", "staged", "resident"])
 def test_host_path_two_batches_in_flight(dev, path):
     """xsknf_gpu_ctx_submit / _wait: batches enqueued back to back (two slots in
     flight, each submit completing the batch two back), contiguous, 2-D-strided
@@ -535,6 +535,45 @@ def test_host_path_two_batches_in_flight(dev, path):
         st = hp.stats()
     assert st["frames"] == b.n
     assert np.array_equal(np.concatenate(outs), ov[perm])
+    assert np.array_equal(umem, ou)
+
+
+@pytest.mark.parametrize("checks", ["zero", "nic"])
+def test_resident_ring(dev, checks):
+    """XSKNF_GPU_PATH_RESIDENT: many small batches through the resident
+    kernel's ring (more in flight than it has entries, so submits wait for old
+    entries), pauses longer than its idle exit (the next submit relaunches it),
+    batches of 1 and of the ring's 1024 frames, one larger batch on the launch
+    path in between; every verdict and byte equals the oracle's."""
+    import time
+    from xsknf_amd import HostPath
+    b = frames.unaligned_batch(12000, "imix", seed=21)
+    if checks == "nic":
+        frames.offload_checks_host(b)
+    frames.inject_edge_cases(b, 0.05, seed=22)
+    ou, ov = run_oracle(b, iters=1, action=O.REDIRECT, nif=2, ingress=1)
+    cs = Checksummer(ChecksummerOptions(action=O.REDIRECT), num_interfaces=2, frame_len_hint=1500)
+    umem = b.umem.copy()
+    rng = np.random.default_rng(23)
+    sizes = [1, 64, 1024, 3000] + list(rng.integers(1, 700, size=40))
+    cuts = [0]
+    for k in sizes:
+        if cuts[-1] + k >= b.n:
+            break
+        cuts.append(cuts[-1] + int(k))
+    cuts.append(b.n)
+    outs = [np.full(hi - lo, 7, dtype=np.int32) for lo, hi in zip(cuts[:-1], cuts[1:])]
+    with HostPath(cs, umem, path="resident", max_batch=8192) as hp:
+        tickets = []
+        for j, ((lo, hi), out) in enumerate(zip(zip(cuts[:-1], cuts[1:]), outs)):
+            tickets.append(hp.submit(b.descs[lo:hi], out, ingress_ifindex=1))
+            if j in (5, 20):            # past the kernel's 5 ms idle exit
+                hp.wait(tickets[-1])
+                time.sleep(0.03)
+        hp.wait(tickets[-1])
+        st = hp.stats()
+    assert st["frames"] == b.n
+    assert np.array_equal(np.concatenate(outs), ov)
     assert np.array_equal(umem, ou)
 
 

@@ -11,7 +11,12 @@
 // Eth/IPv4/UDP frames and drains the tx ring, and counts what the worker
 // received over SECONDS after a half-second warm-up.
 //
-//   hook_bench MODE LEN BATCH SECONDS [ZEROCOPY|STAGED [DEPTH]]   (DEPTH: batches in flight, async)
+//   hook_bench MODE LEN BATCH SECONDS [ZEROCOPY|STAGED|RESIDENT [DEPTH]]   (DEPTH: batches in flight, async)
+//
+// HOOK_BENCH_CHECKS=nic gives the frames the UDP checksums a NIC's offload
+// writes (tests/gen-traffic.lua:120; RFC 768, fully folded), as the reference's
+// traffic carries them: the GPU kernels then write nothing back for all but
+// the carry-loss frames.  Default: random check bytes (every check changes).
 //
 // Prints one JSON line.  Tool, not product: it links the oracle only as the CPU
 // NF of mode "cpu" (the reference path, as tools/config1.py does).
@@ -34,6 +39,21 @@ static int null_nf(void *pkt, unsigned len, unsigned ingress)
 	(void)len;
 	(void)ingress;
 	return 0;
+}
+
+// RFC 768 UDP checksum of an Eth/IPv4 (ihl 5)/UDP frame, as a NIC's offload fills it in
+static uint16_t nic_udp_check(const uint8_t *f, unsigned len)
+{
+	uint64_t s = 17 + ((unsigned)f[38] << 8 | f[39]);
+	for (unsigned i = 26; i < 34; i += 2)
+		s += (unsigned)f[i] << 8 | f[i + 1];
+	for (unsigned i = 34; i < len; i += 2)
+		if (i != 40)
+			s += (unsigned)f[i] << 8 | (i + 1 < len ? f[i + 1] : 0);
+	while (s >> 16)
+		s = (s & 0xffff) + (s >> 16);
+	const uint16_t c = (uint16_t)~s;
+	return c ? c : 0xffff;
 }
 
 static double now_s(void)
@@ -59,7 +79,9 @@ int main(int argc, char **argv)
 	const unsigned len = (unsigned)atoi(argv[2]);
 	const unsigned batch = (unsigned)atoi(argv[3]);
 	const double secs = atof(argv[4]);
-	const int path = argc > 5 && !strcmp(argv[5], "STAGED") ? XSKNF_GPU_PATH_STAGED : XSKNF_GPU_PATH_ZEROCOPY;
+	const int path = argc > 5 && !strcmp(argv[5], "STAGED")     ? XSKNF_GPU_PATH_STAGED
+	                 : argc > 5 && !strcmp(argv[5], "RESIDENT") ? XSKNF_GPU_PATH_RESIDENT
+	                                                            : XSKNF_GPU_PATH_ZEROCOPY;
 	const unsigned depth = argc > 6 ? (unsigned)atoi(argv[6]) : 1;
 	if (len < 42 || len > 3800 || batch == 0) {
 		fprintf(stderr, "bad LEN / BATCH\n");
@@ -108,6 +130,8 @@ int main(int argc, char **argv)
 
 	// frames as tests/gen-traffic.lua builds them (Eth/IPv4 ihl 5/UDP, 256 flows)
 	enum { BURST = 256, TXMAX = 1024, TXSTRIDE = 64 };
+	const char *ck = getenv("HOOK_BENCH_CHECKS");
+	const int nic = ck && !strcmp(ck, "nic");
 	uint8_t *frames = calloc(BURST, len);
 	uint32_t lens[BURST];
 	uint64_t rng = 0x58534B4E;
@@ -125,6 +149,10 @@ int main(int argc, char **argv)
 		f[30] = 172, f[31] = 0, f[32] = 0, f[33] = 1;
 		f[34] = 0x13, f[35] = 0x88, f[36] = 0, f[37] = 80;
 		memcpy(f + 38, &ulen, 2);
+		if (nic) {
+			const uint16_t c = nic_udp_check(f, len);
+			f[40] = (uint8_t)(c >> 8), f[41] = (uint8_t)c;
+		}
 		lens[k] = len;
 	}
 	uint8_t *txbuf = malloc((size_t)TXMAX * TXSTRIDE);
@@ -160,9 +188,11 @@ int main(int argc, char **argv)
 		xsknf_gpu_hook_destroy(hook);
 	xsknf_cleanup();
 	const double mpps = rx / (t1 - tm) / 1e6;
-	printf("{\"mode\": \"%s\", \"len\": %u, \"batch\": %u, \"path\": \"%s\", \"depth\": %u, "
+	printf("{\"checks\": \"%s\", \"mode\": \"%s\", \"len\": %u, \"batch\": %u, \"path\": \"%s\", \"depth\": %u, "
 	       "\"seconds\": %.2f, \"mpps\": %.3f, \"gbps\": %.2f, \"worker_error\": %d}\n",
-	       mode, len, batch, path == XSKNF_GPU_PATH_STAGED ? "STAGED" : "ZEROCOPY", depth, t1 - tm, mpps,
+	       nic ? "nic" : "random", mode, len, batch,
+	       path == XSKNF_GPU_PATH_STAGED ? "STAGED" : path == XSKNF_GPU_PATH_RESIDENT ? "RESIDENT" : "ZEROCOPY",
+	       depth, t1 - tm, mpps,
 	       mpps * len / 1e3, err);
 	free(frames);
 	free(txbuf);

@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
 
 PATH_ZEROCOPY = 0
 PATH_STAGED = 1
+PATH_RESIDENT = 2
 
 ACTION_REDIRECT = 0
 ACTION_DROP = 1

@@ -173,9 +173,10 @@ class HostPath:
     its per-frame loop (:654-672) on the GPU.  `umem` is a host numpy uint8
     array (the worker's mmap), pinned while registered; `process_batch` takes
     host descriptors (DESC_DTYPE) and returns host int32 verdicts, with the check
-    bytes rewritten in `umem`.  path: "zerocopy" or "staged"."""
+    bytes rewritten in `umem`.  path: "zerocopy", "staged" or "resident" (zero-copy,
+    batches of <= 1024 frames through the resident kernel's ring: no launch)."""
 
-    PATHS = {"zerocopy": _lib.PATH_ZEROCOPY, "staged": _lib.PATH_STAGED}
+    PATHS = {"zerocopy": _lib.PATH_ZEROCOPY, "staged": _lib.PATH_STAGED, "resident": _lib.PATH_RESIDENT}
 
     def __init__(self, checksummer: Checksummer, umem, *, path: str = "zerocopy",
                  max_batch: int = 1 << 20, device: int = 0):

@@ -8,7 +8,7 @@
 // (checksummer_user.c:30-112) is replaced by the GPU batch hook of
 // libxsknf_gpu: every rx batch is checksummed by one gfx950 launch.
 //
-// Extra app options: -g, --gpu-path=ZEROCOPY|STAGED (include/xsknf_gpu.h);
+// Extra app options: -g, --gpu-path=ZEROCOPY|STAGED|RESIDENT (include/xsknf_gpu.h);
 // -G, --emu-gen=COUNT[:LEN]: with emulated queues (interfaces "emu<k>", whose
 // kernel side lives in this process) a generator thread plays the reference
 // harness's traffic generator (tests/gen-traffic.lua): COUNT UDP frames of LEN
@@ -68,7 +68,7 @@ static void usage(const char *prog)
 		"  -q, --quiet		Do not display any stats.\n"
 		"  -x, --extra-stats	Display extra statistics.\n"
 		"  -a, --app-stats	Display application (syscall) statistics.\n"
-		"  -g, --gpu-path	ZEROCOPY (default) or STAGED host path to the GPU.\n"
+		"  -g, --gpu-path	ZEROCOPY (default), STAGED or RESIDENT host path to the GPU.\n"
 		"  -s, --gpu-sync	One batch at a time (default: the next batch is received\n"
 		"			while the GPU checksums the last one).\n"
 		"  -d, --gpu-depth	Batches in flight per worker, 1-4 (default 2 for batches\n"
@@ -121,6 +121,8 @@ static void parse_command_line(int argc, char **argv, char *app_path)
 				opt_gpu_path = XSKNF_GPU_PATH_ZEROCOPY;
 			} else if (!strcmp(optarg, "STAGED")) {
 				opt_gpu_path = XSKNF_GPU_PATH_STAGED;
+			} else if (!strcmp(optarg, "RESIDENT")) {
+				opt_gpu_path = XSKNF_GPU_PATH_RESIDENT;
 			} else {
 				fprintf(stderr, "ERROR: invalid gpu path %s\n", optarg);
 				usage(basename(app_path));

@@ -51,4 +51,51 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean = 0);
 void set_error(hipError_t e, const char *where);
 void set_error_text(const char *text);
 
+// ---- the resident worker (XSKNF_GPU_PATH_RESIDENT, host_path.hip) ----------
+// A kernel that stays on the device and takes small batches from a ring in
+// host memory: the host writes a batch's descriptors and header into an entry
+// and publishes its sequence number; block 0 of the kernel polls for it and
+// dispatches it to every block, each block checksums its share (the register
+// kernel's tiles: group_tiles) over PCIe in the mapped UMEM, and the last block
+// to finish publishes `done`.  No launch per batch: the ~10 us launch and
+// completion round trip of a small batch becomes a doorbell and a flag.
+constexpr uint32_t kResSlots = 8;        // ring entries
+constexpr uint32_t kResFrames = 1024;    // frames per entry (larger batches take the launch path)
+constexpr uint32_t kResBlocks = 16;      // blocks of the resident kernel
+constexpr uint64_t kResQuit = ~0ull;
+
+struct alignas(64) ResSlot {   // host memory, coherent and mapped
+  uint64_t seq;                // host -> device: the entry's batch (release), ring sequence numbers from 1
+  uint64_t done;               // device -> host: seq once the batch is complete (release)
+  uint32_t n;
+  int32_t fwd;                 // forward verdict (prepare())
+  uint32_t payload_mult;
+  uint32_t pad[9];
+};
+
+struct alignas(64) ResCtl {    // host memory, coherent and mapped
+  uint64_t stop;               // host -> device: exit now
+  uint64_t pad[7];
+};
+
+struct ResDev {                // device memory, set by the host before each launch
+  uint64_t go;                 // block 0 -> blocks: the highest sequence number dispatched
+  uint64_t quit_at;            // block 0 -> blocks: the first one not processed (kResQuit: running)
+  uint32_t count[kResSlots];   // blocks done with the entry's batch (the last one resets it)
+};
+
+struct ResArgs {
+  KernelArgs base;             // the mapped UMEM and the in-line store modes; n / fwd / mult per batch
+  ResSlot *slots;              // device views of the host arrays
+  xsknf_gpu_desc *descs;       // kResSlots x kResFrames
+  int32_t *verdicts;           // kResSlots x kResFrames
+  ResCtl *ctl;
+  ResDev *dev;
+  uint64_t start;              // first sequence number to process (dev->go = start - 1)
+  uint64_t idle_ticks;         // exit after this long without a batch (100 MHz wall clock) ...
+  uint64_t life_ticks;         // ... or after this long in all; the host relaunches on demand
+};
+
+int launch_resident(const ResArgs &ra, hipStream_t stream);
+
 }  // namespace xsknf_gpu

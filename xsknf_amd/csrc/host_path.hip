@@ -39,11 +39,21 @@
 //   does; the mirror is only read by the kernels, so batches in flight may
 //   share it (their frames are distinct, and a run's gap bytes are the host's
 //   own bytes).
+//
+// RESIDENT: ZEROCOPY, but a batch of at most kResFrames frames does not launch
+//   a kernel: a resident kernel (checksummer.hip resident_kernel) takes it from
+//   a ring in host memory.  submit() writes the descriptors and the entry's
+//   header and publishes its sequence number; wait() spins on the entry's
+//   `done`.  The kernel exits when idle or old (or at destroy) and submit() /
+//   wait() relaunch it from the first entry not done, so a worker pays a
+//   launch only after a pause in its traffic.  Larger batches take the
+//   ZEROCOPY launch path through the slots.
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <algorithm>
 #include <new>
 #include <vector>
@@ -84,6 +94,14 @@ struct Slot {
 
 }  // namespace
 
+struct RingEntry {
+  bool busy = false;
+  uint64_t ticket = 0;                      // the context's sequence number (xsknf_gpu_ctx_wait)
+  uint64_t rseq = 0;                        // the ring's sequence number (ResSlot::seq)
+  uint32_t n = 0;
+  int32_t *out = nullptr;
+};
+
 struct xsknf_gpu_ctx {
   int device = 0;
   int path = XSKNF_GPU_PATH_ZEROCOPY;
@@ -99,6 +117,20 @@ struct xsknf_gpu_ctx {
   int next = 0;                             // slot the next piece goes to (round robin)
   uint64_t seq = 0;                         // pieces submitted
   xsknf_gpu_ctx_stats stats = {};
+  // RESIDENT: the ring (host memory, coherent, mapped) and the kernel's state
+  xsknf_gpu::ResSlot *rslots = nullptr;
+  xsknf_gpu_desc *rdescs = nullptr;
+  int32_t *rverd = nullptr;
+  xsknf_gpu::ResCtl *rctl = nullptr;
+  xsknf_gpu::ResArgs ra = {};               // device views, filled at creation / registration
+  xsknf_gpu::ResDev *rdev = nullptr;
+  xsknf_gpu::ResDev *rinit = nullptr;        // pinned: the state each launch starts from
+  hipStream_t rstream = nullptr;
+  hipEvent_t rdone = nullptr;               // recorded after each launch of the resident kernel
+  bool rlaunched = false;
+  uint64_t rseq = 0;                        // ring entries published
+  RingEntry ring[xsknf_gpu::kResSlots];
+  uint64_t relaunches = 0;
 };
 
 namespace {
@@ -122,6 +154,18 @@ void release(xsknf_gpu_ctx *c) {
     if (s.rec) (void)hipHostFree(s.rec);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
+  if (c->rctl && c->rlaunched) {
+    __atomic_store_n(&c->rctl->stop, 1ull, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(c->rstream);
+  }
+  if (c->rdone) (void)hipEventDestroy(c->rdone);
+  if (c->rstream) (void)hipStreamDestroy(c->rstream);
+  if (c->rslots) (void)hipHostFree(c->rslots);
+  if (c->rdescs) (void)hipHostFree(c->rdescs);
+  if (c->rverd) (void)hipHostFree(c->rverd);
+  if (c->rctl) (void)hipHostFree(c->rctl);
+  if (c->rdev) (void)hipFree(c->rdev);
+  if (c->rinit) (void)hipHostFree(c->rinit);
   if (c->registered) (void)hipHostUnregister(c->umem_host);
   if (c->path == XSKNF_GPU_PATH_STAGED && c->umem_dev) (void)hipFree(c->umem_dev);
   delete c;
@@ -157,14 +201,120 @@ int complete(xsknf_gpu_ctx *c, Slot &s) {
   return 0;
 }
 
-// Complete every piece with a sequence number <= upto, oldest first.
+// ---- RESIDENT: the ring --------------------------------------------------------
+
+constexpr uint64_t kResIdleTicks = 500000;      // 5 ms without a batch (100 MHz wall clock)
+constexpr uint64_t kResLifeTicks = 100000000;   // 1 s
+
+// Launch the resident kernel unless one is running, from the first published
+// entry that is not done (the kernel processes the ring in order, and one that
+// has exited processed every entry it dispatched).
+int ring_launch(xsknf_gpu_ctx *c) {
+  using namespace xsknf_gpu;
+  if (c->rlaunched) {
+    const hipError_t q = hipEventQuery(c->rdone);
+    if (q == hipErrorNotReady) return 0;
+    if (q != hipSuccess) return fail(q, "resident kernel");
+  }
+  uint64_t start = c->rseq + 1;
+  for (const RingEntry &e : c->ring)
+    if (e.busy && __atomic_load_n(&c->rslots[e.rseq % kResSlots].done, __ATOMIC_ACQUIRE) != e.rseq &&
+        e.rseq < start)
+      start = e.rseq;
+  // (the previous launch, and with it the previous copy from rinit, is complete)
+  c->rinit->go = start - 1;
+  c->rinit->quit_at = kResQuit;
+  for (uint32_t &k : c->rinit->count) k = 0;
+  hipError_t e = hipMemcpyAsync(c->rdev, c->rinit, sizeof(ResDev), hipMemcpyHostToDevice, c->rstream);
+  if (e != hipSuccess) return fail(e, "hipMemcpyAsync(resident state)");
+  __atomic_store_n(&c->rctl->stop, 0ull, __ATOMIC_RELEASE);
+  ResArgs ra = c->ra;
+  ra.start = start;
+  ra.idle_ticks = kResIdleTicks;
+  ra.life_ticks = kResLifeTicks;
+  int rc = launch_resident(ra, c->rstream);
+  if (rc) return rc;
+  e = hipEventRecord(c->rdone, c->rstream);
+  if (e != hipSuccess) return fail(e, "hipEventRecord(resident)");
+  c->rlaunched = true;
+  c->relaunches += 1;
+  return 0;
+}
+
+// Wait for a ring entry's batch (relaunching the kernel if it exited before
+// reaching it) and hand out its verdicts.
+int ring_complete(xsknf_gpu_ctx *c, RingEntry &r) {
+  using namespace xsknf_gpu;
+  if (!r.busy) return 0;
+  const xsknf_gpu::ResSlot &h = c->rslots[r.rseq % kResSlots];
+  double t0 = 0;
+  for (uint32_t spin = 1; __atomic_load_n(&h.done, __ATOMIC_ACQUIRE) != r.rseq; ++spin) {
+    __builtin_ia32_pause();
+    if ((spin & 1023) == 0) {
+      timespec ts;
+      clock_gettime(CLOCK_MONOTONIC, &ts);
+      const double t = ts.tv_sec + 1e-9 * ts.tv_nsec;
+      if (!t0) t0 = t;
+      if (t - t0 > 10.0) {   // the kernel relaunches itself within ~1 s: something is wrong
+        xsknf_gpu::set_error_text("resident kernel: no completion within 10 s");
+        return -ETIMEDOUT;
+      }
+      const hipError_t q = hipEventQuery(c->rdone);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(&h.done, __ATOMIC_ACQUIRE) == r.rseq) break;
+        const int rc = ring_launch(c);   // it exited before this entry
+        if (rc) return rc;
+      } else if (q != hipErrorNotReady) {
+        return fail(q, "resident kernel");
+      }
+    }
+  }
+  memcpy(r.out, c->rverd + static_cast<size_t>(r.rseq % kResSlots) * kResFrames, sizeof(int32_t) * r.n);
+  r.busy = false;
+  c->stats.batches += 1;
+  c->stats.frames += r.n;
+  c->stats.bytes_d2h += sizeof(int32_t) * r.n;
+  return 0;
+}
+
+int ring_submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
+                const xsknf_csum_opts *opts, int32_t *verdicts) {
+  using namespace xsknf_gpu;
+  KernelArgs a;
+  int rc = prepare(a, c->umem_dev, c->umem_size, c->ra.descs, n, ingress_ifindex, opts, c->ra.verdicts);
+  if (rc != 0) return rc < 0 ? rc : 0;
+  const uint64_t r = c->rseq + 1;
+  const uint32_t k = static_cast<uint32_t>(r % kResSlots);
+  RingEntry &e = c->ring[k];
+  rc = ring_complete(c, e);   // the entry's previous batch
+  if (rc) return rc;
+  memcpy(c->rdescs + static_cast<size_t>(k) * kResFrames, descs, sizeof(xsknf_gpu_desc) * n);
+  ResSlot &h = c->rslots[k];
+  h.n = n;
+  h.fwd = a.fwd_verdict;
+  h.payload_mult = a.payload_mult;
+  __atomic_store_n(&h.seq, r, __ATOMIC_RELEASE);
+  c->rseq = r;
+  c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
+  e.busy = true;
+  e.ticket = ++c->seq;
+  e.rseq = r;
+  e.n = n;
+  e.out = verdicts;
+  return ring_launch(c);
+}
+
+// Complete every piece / ring batch with a sequence number <= upto, oldest first.
 int complete_upto(xsknf_gpu_ctx *c, uint64_t upto) {
   for (;;) {
     Slot *old = nullptr;
+    RingEntry *rold = nullptr;
     for (Slot &s : c->slot)
       if (s.busy && s.seq <= upto && (!old || s.seq < old->seq)) old = &s;
-    if (!old) return 0;
-    const int rc = complete(c, *old);
+    for (RingEntry &r : c->ring)
+      if (r.busy && r.ticket <= upto && (!rold || r.ticket < rold->ticket)) rold = &r;
+    if (!old && !rold) return 0;
+    const int rc = (rold && (!old || rold->ticket < old->seq)) ? ring_complete(c, *rold) : complete(c, *old);
     if (rc) return rc;
   }
 }
@@ -278,7 +428,7 @@ int submit_piece(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint
 
   xsknf_gpu_launch_cfg cfg;
   default_cfg(c->hint ? c->hint : 2048u, cfg);
-  bool mapped = c->path == XSKNF_GPU_PATH_ZEROCOPY;
+  bool mapped = c->path != XSKNF_GPU_PATH_STAGED;
   if (!mapped) {
     rc = stage_frames(c, s, n, a);
     if (rc < 0) return rc;
@@ -311,6 +461,12 @@ int submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint32_t i
   if (n && (!descs || !verdicts)) return -EINVAL;
   hipError_t e = hipSetDevice(c->device);
   if (e != hipSuccess) return fail(e, "hipSetDevice");
+  if (c->path == XSKNF_GPU_PATH_RESIDENT && n > 0 && n <= xsknf_gpu::kResFrames) {
+    const int rc = ring_submit(c, descs, n, ingress_ifindex, opts, verdicts);
+    if (rc) return rc;
+    if (ticket) *ticket = c->seq;
+    return 0;
+  }
   for (uint32_t p = 0; p < n; p += c->slot_frames) {
     const uint32_t k = std::min(c->slot_frames, n - p);
     const int rc = submit_piece(c, descs + p, k, ingress_ifindex, opts, verdicts + p);
@@ -333,7 +489,8 @@ extern "C" {
 int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint32_t max_batch,
                          uint32_t frame_len_hint) {
   if (!out || max_batch == 0) return -EINVAL;
-  if (path != XSKNF_GPU_PATH_ZEROCOPY && path != XSKNF_GPU_PATH_STAGED) return -EINVAL;
+  if (path != XSKNF_GPU_PATH_ZEROCOPY && path != XSKNF_GPU_PATH_STAGED && path != XSKNF_GPU_PATH_RESIDENT)
+    return -EINVAL;
   *out = nullptr;
   xsknf_gpu_ctx *c = new (std::nothrow) xsknf_gpu_ctx;
   if (!c) return -ENOMEM;
@@ -350,6 +507,27 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
     if (e == hipSuccess) e = hipHostMalloc(&s.rec, sizeof(int32_t) * c->slot_frames, hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.descs_mapped), s.descs, 0);
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.rec_mapped), s.rec, 0);
+  }
+  if (e == hipSuccess && path == XSKNF_GPU_PATH_RESIDENT) {
+    using namespace xsknf_gpu;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    e = hipHostMalloc(&c->rslots, sizeof(ResSlot) * kResSlots, fl);
+    if (e == hipSuccess) e = hipHostMalloc(&c->rdescs, sizeof(xsknf_gpu_desc) * kResSlots * kResFrames, fl);
+    if (e == hipSuccess) e = hipHostMalloc(&c->rverd, sizeof(int32_t) * kResSlots * kResFrames, fl);
+    if (e == hipSuccess) e = hipHostMalloc(&c->rctl, sizeof(ResCtl), fl);
+    if (e == hipSuccess) e = hipMalloc(&c->rdev, sizeof(ResDev));
+    if (e == hipSuccess) e = hipHostMalloc(&c->rinit, sizeof(ResDev), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->rdone, hipEventDisableTiming);
+    if (e == hipSuccess) {
+      memset(c->rslots, 0, sizeof(ResSlot) * kResSlots);
+      memset(c->rctl, 0, sizeof(ResCtl));
+      e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.slots), c->rslots, 0);
+    }
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.descs), c->rdescs, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.verdicts), c->rverd, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.ctl), c->rctl, 0);
+    c->ra.dev = c->rdev;
   }
   if (e != hipSuccess) {
     const int rc = fail(e, "xsknf_gpu_ctx_create");
@@ -372,7 +550,7 @@ int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *c, void *umem, uint64_t si
   e = hipHostGetDevicePointer(&dp, umem, 0);
   c->umem_mapped = static_cast<uint8_t *>(dp);
   if (e == hipSuccess) {
-    if (c->path == XSKNF_GPU_PATH_ZEROCOPY)
+    if (c->path != XSKNF_GPU_PATH_STAGED)
       c->umem_dev = c->umem_mapped;
     else
       e = hipMalloc(&c->umem_dev, size + 16);   // + the last chunk's 16-byte read
@@ -382,6 +560,16 @@ int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *c, void *umem, uint64_t si
     c->registered = false;
     c->umem_dev = c->umem_mapped = nullptr;
     return fail(e, "xsknf_gpu_ctx_register_umem");
+  }
+  if (c->path == XSKNF_GPU_PATH_RESIDENT) {
+    // the resident kernel's fixed arguments: the mapped UMEM, checks in-line as
+    // 2-byte stores (host memory has byte enables), per-batch fields from the ring
+    using namespace xsknf_gpu;
+    const xsknf_csum_opts o = {1, XSKNF_CSUM_ACTION_DROP, 1, 0};
+    KernelArgs &a = c->ra.base;
+    (void)prepare(a, c->umem_dev, c->umem_size, c->ra.descs, 1, 0, &o, c->ra.verdicts);
+    a.defer_min_len = kNoDefer;
+    a.sector_stores = 0;
   }
   return 0;
 }
@@ -460,7 +648,8 @@ extern "C" {
 int xsknf_gpu_hook_create(struct xsknf_gpu_hook **out, const struct xsknf_csum_opts *opts, uint32_t workers,
                           int path, uint32_t max_batch, uint32_t frame_len_hint) {
   if (!out || !opts || workers == 0 || max_batch == 0) return -EINVAL;
-  if (path != XSKNF_GPU_PATH_ZEROCOPY && path != XSKNF_GPU_PATH_STAGED) return -EINVAL;
+  if (path != XSKNF_GPU_PATH_ZEROCOPY && path != XSKNF_GPU_PATH_STAGED && path != XSKNF_GPU_PATH_RESIDENT)
+    return -EINVAL;
   if (opts->action != XSKNF_CSUM_ACTION_REDIRECT && opts->action != XSKNF_CSUM_ACTION_DROP) return -EINVAL;
   *out = nullptr;
   int devices = 0;
