@@ -195,14 +195,18 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            the 4-byte records come back and the host writes
  *                            the 2 check bytes.  A batch of frames scattered
  *                            over the UMEM runs as ZEROCOPY instead.
- *   XSKNF_GPU_PATH_RESIDENT  ZEROCOPY, but a batch of at most 1024 frames
- *                            launches nothing: a kernel resident on the device
- *                            takes it from a ring in host memory (the submit
- *                            writes the descriptors and rings a doorbell, the
- *                            wait spins on a completion flag), for the rx loop's
- *                            small batches.  The kernel leaves after 5 ms
- *                            without a batch (and after 1 s in all) and is
- *                            relaunched by the next submit or wait.
+ *   XSKNF_GPU_PATH_RESIDENT  ZEROCOPY without a launch per batch: a kernel
+ *                            resident on the device takes the batches from a
+ *                            ring in host memory (the submit writes the
+ *                            descriptors and rings a doorbell, the wait spins
+ *                            on a completion flag), 8 entries of up to 256
+ *                            frames, one block each, so up to 8 batches (or
+ *                            pieces of a larger one) are processed at once.
+ *                            For the rx loop's small batches.  The kernel leaves
+ *                            after 5 ms without a batch (and after 1 s in all)
+ *                            and the next submit or wait relaunches it.  It
+ *                            holds a hardware queue: at most 3 RESIDENT
+ *                            contexts per device, further ones run as ZEROCOPY.
  * One context = one worker thread.  It keeps up to five batches in flight (five slots,
  * each with its own HIP stream; XSKNF_MAX_HOOK_DEPTH batches out plus the one being
  * submitted): the copies and kernel of one overlap another's, and the host's share

@@ -2096,91 +2096,72 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
 
 // ---- the resident worker (checksummer_internal.h) ------------------------------
 //
-// Block 0's first lane polls the ring entry of the next sequence number in
-// host memory (system-scope acquire loads: vector loads that bypass the
-// caches) and dispatches it to the blocks through `dev->go` in device memory;
-// every block checksums its share of the batch (the register kernel's tiles
-// with 32 lanes x 3 chunks per frame -- the launch path's small-batch shape over
-// PCIe, host_path.hip pcie_small_batch_cfg), and the last block to finish
-// stores `done` to host memory (system-scope release).  The kernel exits when
-// the host sets ctl->stop, after idle_ticks without a batch or after
-// life_ticks in all: block 0 then publishes quit_at, the first sequence number
-// no block will process, so every dispatched batch is processed by all blocks
-// or by none (the host relaunches from the first entry not done).  Blocks that
-// never hear from block 0 (it could not be scheduled) give up after twice the
-// lifetime: every wave reaches an exit.
-constexpr int kResLpf = 32, kResNch = 3, kResSpt = 2;
+// Block b owns ring entry b: its first lane polls the entry in host memory for
+// the next sequence number that maps to it (system-scope acquire loads: vector
+// loads that bypass the caches), the block checksums the batch (the register
+// kernel's tiles, 8 lanes x 12 chunks per frame: a frame of up to 1536 B in one
+// pass, the whole batch in one or two rounds of PCIe reads), and the first
+// lane stores `done` to host memory (system-scope release).  A block leaves
+// when the host sets ctl->stop, after idle_ticks without a batch or after
+// life_ticks in all, and tells the others through dev->quit; a batch published
+// for a block that left waits for the host to relaunch the kernel (each block
+// then starts at its entry's first batch not done).  Every wave reaches an
+// exit: the poll loops are bounded by the clock, and a batch is a bounded loop.
+constexpr int kResLpf = 8, kResNch = 12, kResSpt = 2;
 
 __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
   __shared__ uint64_t cmd;
   __shared__ uint32_t hdr[3];
+  const uint32_t b = blockIdx.x;
+  ResSlot &e = ra.slots[b];
   const uint64_t t0 = wall_clock64();
   uint64_t last = t0;
-  for (uint64_t next = ra.start;; ++next) {
+  for (uint64_t seq = ra.start[b];; seq += kResSlots) {
     if (threadIdx.x == 0) {
       uint64_t c = kResQuit;
-      if (blockIdx.x == 0) {
-        ResSlot &e = ra.slots[next % kResSlots];
+      {
         for (;;) {
-          if (__hip_atomic_load(&e.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == next) {
-            c = next;
+          if (__hip_atomic_load(&e.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == seq) {
+            c = seq;
             break;
           }
           const uint64_t now = wall_clock64();
-          if (__hip_atomic_load(&ra.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-              now - last > ra.idle_ticks || now - t0 > ra.life_ticks)
-            break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-        if (c == kResQuit)
-          __hip_atomic_store(&ra.dev->quit_at, next, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          __hip_atomic_store(&ra.dev->go, next, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        for (;;) {
-          if (__hip_atomic_load(&ra.dev->go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= next) {
-            c = next;
+          if (__hip_atomic_load(&ra.dev->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+              __hip_atomic_load(&ra.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+              now - last > ra.idle_ticks || now - t0 > ra.life_ticks) {
+            __hip_atomic_store(&ra.dev->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
-          if (__hip_atomic_load(&ra.dev->quit_at, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <= next ||
-              wall_clock64() - t0 > 2 * ra.life_ticks + ra.idle_ticks)
-            break;
           __builtin_amdgcn_s_sleep(2);
         }
-      }
-      if (c != kResQuit) {
-        // the host's writes of this batch (header, descriptors, frames), seen from this CU
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
-        ResSlot &e = ra.slots[c % kResSlots];
-        hdr[0] = __hip_atomic_load(&e.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        hdr[1] = static_cast<uint32_t>(__hip_atomic_load(&e.fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        hdr[2] = __hip_atomic_load(&e.payload_mult, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (c != kResQuit) {
+          // the host's writes of this batch (header, descriptors, frames), seen from this CU
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
+          hdr[0] = __hip_atomic_load(&e.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          hdr[1] = static_cast<uint32_t>(__hip_atomic_load(&e.fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+          hdr[2] = __hip_atomic_load(&e.payload_mult, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
       }
       cmd = c;
     }
     __syncthreads();
     const uint64_t c = cmd;
     if (c == kResQuit) break;
-    const uint32_t sl = static_cast<uint32_t>(c % kResSlots);
-    KernelArgs a = ra.base;
-    a.descs = ra.descs + static_cast<size_t>(sl) * kResFrames;
-    a.verdicts = ra.verdicts + static_cast<size_t>(sl) * kResFrames;
-    a.n = min(hdr[0], kResFrames);
-    a.fwd_verdict = static_cast<int32_t>(hdr[1]);
-    a.payload_mult = hdr[2];
-    if (a.n) group_tiles<kResLpf, kResNch, kResSpt>(a, blockIdx.x, gridDim.x);
-    __syncthreads();   // this block's stores are issued and done (workgroup release / acquire)
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the block's checks and verdicts
-      const uint32_t prev = __hip_atomic_fetch_add(&ra.dev->count[sl], 1u, __ATOMIC_ACQ_REL,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == gridDim.x - 1) {
-        __hip_atomic_store(&ra.dev->count[sl], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&ra.slots[sl].done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    {
+      KernelArgs a = ra.base;
+      a.descs = ra.descs + static_cast<size_t>(b) * kResFrames;
+      a.verdicts = ra.verdicts + static_cast<size_t>(b) * kResFrames;
+      a.n = min(hdr[0], kResFrames);
+      a.fwd_verdict = static_cast<int32_t>(hdr[1]);
+      a.payload_mult = hdr[2];
+      if (a.n) group_tiles<kResLpf, kResNch, kResSpt>(a, 0, 1);
+      __syncthreads();   // the block's stores are done (workgroup release / acquire)
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
+        __hip_atomic_store(&e.done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = wall_clock64();
       }
-      last = wall_clock64();
     }
-    __syncthreads();   // hdr / cmd are rewritten for the next batch
   }
 }
 
@@ -2252,7 +2233,7 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
 }
 
 int launch_resident(const ResArgs &ra, hipStream_t stream) {
-  hipLaunchKernelGGL(resident_kernel, dim3(kResBlocks), dim3(kBlock), 0, stream, ra);
+  hipLaunchKernelGGL(resident_kernel, dim3(kResSlots), dim3(kBlock), 0, stream, ra);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_error(e, "resident_kernel launch"); return -EIO; }
   return 0;

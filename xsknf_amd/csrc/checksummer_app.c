@@ -37,7 +37,7 @@
 static int opt_action = XSKNF_CSUM_ACTION_REDIRECT;
 static int opt_csum_iterations = 1;
 static int opt_quiet, opt_extra_stats, opt_app_stats;
-static int opt_gpu_path = XSKNF_GPU_PATH_ZEROCOPY;
+static int opt_gpu_path = -1;   // -1: by batch size (RESIDENT up to 128 frames, else ZEROCOPY)
 static int opt_gpu_sync;
 static int opt_gpu_depth;   // 0: by batch size
 static unsigned long opt_gen_count;
@@ -68,7 +68,8 @@ static void usage(const char *prog)
 		"  -q, --quiet		Do not display any stats.\n"
 		"  -x, --extra-stats	Display extra statistics.\n"
 		"  -a, --app-stats	Display application (syscall) statistics.\n"
-		"  -g, --gpu-path	ZEROCOPY (default), STAGED or RESIDENT host path to the GPU.\n"
+		"  -g, --gpu-path	ZEROCOPY, STAGED or RESIDENT host path to the GPU\n"
+		"			(default: RESIDENT for batches of up to 128 frames, else ZEROCOPY).\n"
 		"  -s, --gpu-sync	One batch at a time (default: the next batch is received\n"
 		"			while the GPU checksums the last one).\n"
 		"  -d, --gpu-depth	Batches in flight per worker, 1-4 (default 2 for batches\n"
@@ -343,6 +344,12 @@ int main(int argc, char **argv)
 		.num_interfaces = config.num_interfaces,
 	};
 	struct xsknf_gpu_hook *hook = NULL;
+	// small rx batches (the reference's default is 64, src/xsknf.c:49): the
+	// resident kernel's ring, four batches out (NF level, 64 B frames: 19 vs
+	// 12 Mpps for launched batches; 1500 B: 17 vs 9 -- DESIGN 5.3)
+	const int small = config.batch_size <= 128;
+	if (opt_gpu_path < 0)
+		opt_gpu_path = small ? XSKNF_GPU_PATH_RESIDENT : XSKNF_GPU_PATH_ZEROCOPY;
 	rc = xsknf_gpu_hook_create(&hook, &opts, config.workers, opt_gpu_path, config.batch_size,
 			(uint32_t)config.xsk_frame_size);
 	if (rc) {
@@ -357,7 +364,8 @@ int main(int argc, char **argv)
 				(xsknf_batch_complete_fn)xsknf_gpu_hook_complete, hook);
 	// two in flight pay at the reference's small batches, not from 256 frames on
 	// (tools/hook_bench.c: 1500 B x 64 5.8 -> 8.2 Mpps, x 256 13.2 -> 11.8)
-	xsknf_set_batch_depth(opt_gpu_depth ? (unsigned)opt_gpu_depth : (config.batch_size <= 128 ? 2u : 1u));
+	xsknf_set_batch_depth(opt_gpu_depth ? (unsigned)opt_gpu_depth
+	                                    : opt_gpu_path == XSKNF_GPU_PATH_RESIDENT ? 4u : (small ? 2u : 1u));
 	rc = xsknf_start_workers();
 	if (rc) {
 		fprintf(stderr, "ERROR: xsknf_start_workers: %s\n", strerror(-rc));

@@ -53,24 +53,24 @@ void set_error_text(const char *text);
 
 // ---- the resident worker (XSKNF_GPU_PATH_RESIDENT, host_path.hip) ----------
 // A kernel that stays on the device and takes small batches from a ring in
-// host memory: the host writes a batch's descriptors and header into an entry
-// and publishes its sequence number; block 0 of the kernel polls for it and
-// dispatches it to every block, each block checksums its share (the register
-// kernel's tiles: group_tiles) over PCIe in the mapped UMEM, and the last block
-// to finish publishes `done`.  No launch per batch: the ~10 us launch and
-// completion round trip of a small batch becomes a doorbell and a flag.
-constexpr uint32_t kResSlots = 8;        // ring entries
-constexpr uint32_t kResFrames = 1024;    // frames per entry (larger batches take the launch path)
-constexpr uint32_t kResBlocks = 16;      // blocks of the resident kernel
+// host memory, one 4-wave block per ring entry: the host writes a batch's
+// descriptors and header into entry seq % kResSlots and publishes seq; the
+// entry's block polls for it, checksums the batch over PCIe in the mapped UMEM
+// (the register kernel's tiles: group_tiles) and publishes `done`.  No launch
+// per batch, and up to kResSlots batches in flight at once: the ~10 us launch
+// and completion round trip of a small batch becomes a doorbell and a flag.
+constexpr uint32_t kResSlots = 8;        // ring entries = blocks of the resident kernel
+constexpr uint32_t kResFrames = 256;     // frames per entry (larger batches take the launch path)
 constexpr uint64_t kResQuit = ~0ull;
 
 struct alignas(64) ResSlot {   // host memory, coherent and mapped
   uint64_t seq;                // host -> device: the entry's batch (release), ring sequence numbers from 1
-  uint64_t done;               // device -> host: seq once the batch is complete (release)
-  uint32_t n;
+  uint32_t n;                  // written before seq
   int32_t fwd;                 // forward verdict (prepare())
   uint32_t payload_mult;
-  uint32_t pad[9];
+  uint32_t pad1;
+  uint64_t done;               // device -> host: seq once the batch is complete (release)
+  uint32_t pad[8];
 };
 
 struct alignas(64) ResCtl {    // host memory, coherent and mapped
@@ -78,10 +78,8 @@ struct alignas(64) ResCtl {    // host memory, coherent and mapped
   uint64_t pad[7];
 };
 
-struct ResDev {                // device memory, set by the host before each launch
-  uint64_t go;                 // block 0 -> blocks: the highest sequence number dispatched
-  uint64_t quit_at;            // block 0 -> blocks: the first one not processed (kResQuit: running)
-  uint32_t count[kResSlots];   // blocks done with the entry's batch (the last one resets it)
+struct ResDev {                // device memory, zeroed by the host before each launch
+  uint32_t quit;               // a block has left: every block leaves at its next poll
 };
 
 struct ResArgs {
@@ -91,7 +89,7 @@ struct ResArgs {
   int32_t *verdicts;           // kResSlots x kResFrames
   ResCtl *ctl;
   ResDev *dev;
-  uint64_t start;              // first sequence number to process (dev->go = start - 1)
+  uint64_t start[kResSlots];   // per entry: the first sequence number its block processes
   uint64_t idle_ticks;         // exit after this long without a batch (100 MHz wall clock) ...
   uint64_t life_ticks;         // ... or after this long in all; the host relaunches on demand
 };

@@ -42,12 +42,14 @@
 //
 // RESIDENT: ZEROCOPY, but a batch of at most kResFrames frames does not launch
 //   a kernel: a resident kernel (checksummer.hip resident_kernel) takes it from
-//   a ring in host memory.  submit() writes the descriptors and the entry's
+//   a ring in host memory (one 4-wave block per entry, so up to eight batches
+//   are processed at once).  submit() writes the descriptors and the entry's
 //   header and publishes its sequence number; wait() spins on the entry's
 //   `done`.  The kernel exits when idle or old (or at destroy) and submit() /
 //   wait() relaunch it from the first entry not done, so a worker pays a
-//   launch only after a pause in its traffic.  Larger batches take the
-//   ZEROCOPY launch path through the slots.
+//   launch only after a pause in its traffic.  A batch larger than an entry
+//   takes several entries (blocks) at once; no batch takes the launch path,
+//   whose kernels could queue behind the resident one (resident_acquire).
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
@@ -55,6 +57,7 @@
 #include <string.h>
 #include <time.h>
 #include <algorithm>
+#include <atomic>
 #include <new>
 #include <vector>
 
@@ -135,6 +138,22 @@ struct xsknf_gpu_ctx {
 
 namespace {
 
+// A resident kernel holds its hardware queue, and streams beyond the device's
+// hardware queues (GPU_MAX_HW_QUEUES, 4 by default) share them: a launch on a
+// stream sharing the queue would wait behind the resident kernel until it
+// idles out.  So at most kMaxResident RESIDENT contexts per device (one
+// stream each); further ones run as ZEROCOPY.
+constexpr int kMaxResident = 3;
+std::atomic<int> g_resident[64];
+
+bool resident_acquire(int device) {
+  if (device < 0 || device >= 64) return false;
+  int v = g_resident[device].load();
+  while (v < kMaxResident)
+    if (g_resident[device].compare_exchange_weak(v, v + 1)) return true;
+  return false;
+}
+
 int fail(hipError_t e, const char *where) {
   xsknf_gpu::set_error(e, where);
   return -EIO;
@@ -158,6 +177,7 @@ void release(xsknf_gpu_ctx *c) {
     __atomic_store_n(&c->rctl->stop, 1ull, __ATOMIC_RELEASE);
     (void)hipStreamSynchronize(c->rstream);
   }
+  if (c->path == XSKNF_GPU_PATH_RESIDENT && c->device >= 0 && c->device < 64) g_resident[c->device].fetch_sub(1);
   if (c->rdone) (void)hipEventDestroy(c->rdone);
   if (c->rstream) (void)hipStreamDestroy(c->rstream);
   if (c->rslots) (void)hipHostFree(c->rslots);
@@ -206,9 +226,9 @@ int complete(xsknf_gpu_ctx *c, Slot &s) {
 constexpr uint64_t kResIdleTicks = 500000;      // 5 ms without a batch (100 MHz wall clock)
 constexpr uint64_t kResLifeTicks = 100000000;   // 1 s
 
-// Launch the resident kernel unless one is running, from the first published
-// entry that is not done (the kernel processes the ring in order, and one that
-// has exited processed every entry it dispatched).
+// Launch the resident kernel unless one is running.  Block b starts at entry
+// b's batch if that is published and not done, else at the entry's next
+// sequence number (a block that left has finished every batch it took).
 int ring_launch(xsknf_gpu_ctx *c) {
   using namespace xsknf_gpu;
   if (c->rlaunched) {
@@ -216,20 +236,21 @@ int ring_launch(xsknf_gpu_ctx *c) {
     if (q == hipErrorNotReady) return 0;
     if (q != hipSuccess) return fail(q, "resident kernel");
   }
-  uint64_t start = c->rseq + 1;
-  for (const RingEntry &e : c->ring)
-    if (e.busy && __atomic_load_n(&c->rslots[e.rseq % kResSlots].done, __ATOMIC_ACQUIRE) != e.rseq &&
-        e.rseq < start)
-      start = e.rseq;
+  ResArgs ra = c->ra;
+  for (uint32_t b = 0; b < kResSlots; ++b) {
+    const RingEntry &e = c->ring[b];
+    if (e.rseq == 0)
+      ra.start[b] = b ? b : kResSlots;   // the entry's first sequence number (they start at 1)
+    else if (__atomic_load_n(&c->rslots[b].done, __ATOMIC_ACQUIRE) == e.rseq)
+      ra.start[b] = e.rseq + kResSlots;
+    else
+      ra.start[b] = e.rseq;
+  }
   // (the previous launch, and with it the previous copy from rinit, is complete)
-  c->rinit->go = start - 1;
-  c->rinit->quit_at = kResQuit;
-  for (uint32_t &k : c->rinit->count) k = 0;
+  c->rinit->quit = 0;
   hipError_t e = hipMemcpyAsync(c->rdev, c->rinit, sizeof(ResDev), hipMemcpyHostToDevice, c->rstream);
   if (e != hipSuccess) return fail(e, "hipMemcpyAsync(resident state)");
   __atomic_store_n(&c->rctl->stop, 0ull, __ATOMIC_RELEASE);
-  ResArgs ra = c->ra;
-  ra.start = start;
   ra.idle_ticks = kResIdleTicks;
   ra.life_ticks = kResLifeTicks;
   int rc = launch_resident(ra, c->rstream);
@@ -461,9 +482,17 @@ int submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint32_t i
   if (n && (!descs || !verdicts)) return -EINVAL;
   hipError_t e = hipSetDevice(c->device);
   if (e != hipSuccess) return fail(e, "hipSetDevice");
-  if (c->path == XSKNF_GPU_PATH_RESIDENT && n > 0 && n <= xsknf_gpu::kResFrames) {
-    const int rc = ring_submit(c, descs, n, ingress_ifindex, opts, verdicts);
-    if (rc) return rc;
+  if (c->path == XSKNF_GPU_PATH_RESIDENT) {
+    // every batch through the ring, in entries of up to kResFrames frames (a
+    // larger batch is processed by several blocks at once)
+    for (uint32_t p = 0; p < n; p += xsknf_gpu::kResFrames) {
+      const uint32_t k = std::min(xsknf_gpu::kResFrames, n - p);
+      const int rc = ring_submit(c, descs + p, k, ingress_ifindex, opts, verdicts + p);
+      if (rc) {
+        if (p) (void)complete_upto(c, c->seq);
+        return rc;
+      }
+    }
     if (ticket) *ticket = c->seq;
     return 0;
   }
@@ -500,7 +529,9 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
   c->slot_frames = std::min(max_batch, kPiece);
   c->hint = frame_len_hint;
   hipError_t e = hipSetDevice(device);
+  if (path == XSKNF_GPU_PATH_RESIDENT && !resident_acquire(device)) c->path = path = XSKNF_GPU_PATH_ZEROCOPY;
   for (Slot &s : c->slot) {
+    if (path == XSKNF_GPU_PATH_RESIDENT) break;   // the ring takes every batch
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipHostMalloc(&s.descs, sizeof(xsknf_gpu_desc) * c->slot_frames, hipHostMallocDefault);
