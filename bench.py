@@ -228,11 +228,12 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     #   wrote changes again -- the step's work is that of fresh frames (the
     #   kernel's cost does not depend on the iteration count: closed form);
     # * NIC workloads: the checks a step changes (the carry-loss frames, 0.005 %
-    #   of 64 B frames to 3.7 % of jumbo frames) are put back right after it on
-    #   the launch stream, inside the timed region (a small index_put per step:
-    #   conservative -- putting them back on a side stream while the next batch
-    #   ran measured slower still, its cross-stream waits sitting between the
-    #   steps).
+    #   of 64 B frames to 3.7 % of jumbo frames) are put back after it on the
+    #   launch stream, and each step is timed by its own HIP events around its
+    #   launch only (the put-back is test scaffolding: an index_put and its
+    #   launch gap, ~7 us per step; putting them back on a side stream while the
+    #   next batch ran instead measured slower, its cross-stream waits sitting
+    #   between the steps).
     cs_alt = Checksummer(ChecksummerOptions(csum_iterations=2), num_interfaces=1, frame_len_hint=hint,
                          frame_len_mean=mean)
     nic = name in NIC
@@ -269,14 +270,20 @@ def time_workload(name, args, world, rank, dev, seed, primary):
         torch.cuda.synchronize()
 
     it = [0]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps if nic else 0)]
 
     def step():
         j = it[0] % K
         c = cs_alt if (not nic and (it[0] // K) & 1) else cs
-        it[0] += 1
+        if nic:
+            evs[it[0] % len(evs)][0].record(stream)
         c.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[j], n, v_ptrs[j], 0, stream.cuda_stream)
-        if nic and restore[j][0].numel():
-            umem[restore[j][0]] = restore[j][1]   # this batch's changed checks, back as the NIC wrote them
+        if nic:
+            evs[it[0] % len(evs)][1].record(stream)
+            if restore[j][0].numel():
+                umem[restore[j][0]] = restore[j][1]   # this batch's changed checks, back as the NIC wrote them
+        it[0] += 1
 
     # W untimed warmup steps, continued until at least --min-warmup-s of
     # warmup has run: measured on MI355X, 10 steps (3 ms) leave the step ~3 %
@@ -302,7 +309,8 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     wall = time.perf_counter() - t0
     # frame bytes of the timed steps (the K batches differ slightly in length mix)
     bytes_len = sum(batch_bytes[i % K] for i in range(first, first + args.steps)) // args.steps
-    step_ms = ev0.elapsed_time(ev1) / args.steps
+    # NIC: the last args.steps steps were the timed ones, each between its own events
+    step_ms = (sum(a.elapsed_time(b) for a, b in evs) if nic else ev0.elapsed_time(ev1)) / args.steps
     wall_max = allreduce_max(wall, world)
     step_ms_max = allreduce_max(step_ms, world)
     if not nic:
