@@ -96,6 +96,9 @@ def parse():
     p.add_argument("--rotate", type=int, default=0,
                    help="batches the steps cycle through (0 = enough to exceed --rotate-bytes)")
     p.add_argument("--rotate-bytes", type=int, default=1 << 30)
+    p.add_argument("--streams", type=int, default=1,
+                   help="launch streams the steps rotate over (batches are independent: with 2, one batch's "
+                        "launch starts while the previous one drains; needs >= 2 rotated batches)")
     p.add_argument("--kernel-steps", type=int, default=50,
                    help="launches of the summing kernel alone (records only), reported beside the step")
     return p.parse_args()
@@ -210,6 +213,11 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     lens_in, span = workload_lengths(name, args, world, rank)
     n = int(lens_in.shape[0])
     K = rotation(lens_in, args)
+    S = args.streams if name not in NIC else 1
+    if S > 1:
+        # steps in flight together own distinct batches, and every visit of a
+        # batch goes to the same stream (K a multiple of S), so visits stay ordered
+        K = -(-max(K, S) // S) * S
     # K batches of the same shape in one UMEM (batch j = frames [j*n, (j+1)*n)),
     # step i processes batch i % K
     umem, descs, lens = frames.device_batch(n * K, np.tile(lens_in, K), layout=layout, chunk=chunk or frames.CHUNK,
@@ -269,6 +277,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
         del addr, starts, at, orig
         torch.cuda.synchronize()
 
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     it = [0]
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps if nic else 0)]
@@ -278,7 +287,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
         c = cs_alt if (not nic and (it[0] // K) & 1) else cs
         if nic:
             evs[it[0] % len(evs)][0].record(stream)
-        c.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[j], n, v_ptrs[j], 0, stream.cuda_stream)
+        c.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[j], n, v_ptrs[j], 0, streams[it[0] % S].cuda_stream)
         if nic:
             evs[it[0] % len(evs)][1].record(stream)
             if restore[j][0].numel():
@@ -302,8 +311,14 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     t0 = time.perf_counter()
     first = it[0]
     ev0.record(stream)
+    for st in streams[1:]:
+        st.wait_event(ev0)
     for _ in range(args.steps):
         step()
+    for st in streams[1:]:
+        e = torch.cuda.Event()
+        e.record(st)
+        stream.wait_event(e)
     ev1.record(stream)
     barrier(world)
     wall = time.perf_counter() - t0
