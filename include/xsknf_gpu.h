@@ -203,10 +203,12 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            frames, one block each, so up to 8 batches (or
  *                            pieces of a larger one) are processed at once.
  *                            For the rx loop's small batches.  The kernel leaves
- *                            after 5 ms without a batch (and after 1 s in all)
- *                            and the next submit or wait relaunches it.  It
- *                            holds a hardware queue: at most 3 RESIDENT
- *                            contexts per device, further ones run as ZEROCOPY.
+ *                            after 1 ms without a batch (and after 4 ms in all)
+ *                            and the next submit or wait relaunches it: it holds
+ *                            a hardware queue, and work queued behind it on a
+ *                            stream sharing that queue waits at most that long.
+ *                            At most 3 RESIDENT contexts per device; further
+ *                            ones run as ZEROCOPY.
  * One context = one worker thread.  It keeps up to five batches in flight (five slots,
  * each with its own HIP stream; XSKNF_MAX_HOOK_DEPTH batches out plus the one being
  * submitted): the copies and kernel of one overlap another's, and the host's share

@@ -577,6 +577,35 @@ def test_resident_ring(dev, checks):
     assert np.array_equal(umem, ou)
 
 
+def test_resident_contexts_past_the_limit_run_zerocopy(dev):
+    """Five RESIDENT contexts on one device at once, batches interleaved over
+    them: the first three hold resident kernels (each a hardware queue), the
+    others run as ZEROCOPY (include/xsknf_gpu.h); every context's frames come
+    out equal to the oracle's."""
+    from xsknf_amd import HostPath
+    bs = [frames.aligned_batch(2000, "imix", chunk=2048, seed=40 + k) for k in range(5)]
+    for k, b in enumerate(bs):
+        frames.inject_edge_cases(b, 0.05, seed=50 + k)
+    refs = [run_oracle(b, iters=1, action=O.DROP, nif=1) for b in bs]
+    cs = Checksummer(ChecksummerOptions(action=O.DROP), frame_len_hint=1500)
+    umems = [b.umem.copy() for b in bs]
+    hps = [HostPath(cs, u, path="resident", max_batch=2000) for u in umems]
+    try:
+        outs = [np.full(b.n, 7, dtype=np.int32) for b in bs]
+        tickets = [[] for _ in bs]
+        for lo in range(0, 2000, 100):
+            for k, (hp, b) in enumerate(zip(hps, bs)):
+                tickets[k].append(hp.submit(b.descs[lo:lo + 100], outs[k][lo:lo + 100]))
+        for hp, t in zip(hps, tickets):
+            hp.wait(t[-1])
+    finally:
+        for hp in hps:
+            hp.close()
+    for (ou, ov), u, v in zip(refs, umems, outs):
+        assert np.array_equal(v, ov)
+        assert np.array_equal(u, ou)
+
+
 @pytest.mark.parametrize("shape", [(16, 2, 2, 0, 1, 1, 20), (16, 3, 1, 0, 0, 1, 24), (16, 3, 2, 0, 2, 1, 20),
                                    (16, 2, 2, 0, 5, 1, 24)], ids=["w4-16x2", "w8-16x3", "w4-16x3u2", "w8-16x2-2B"])
 def test_huge_frames_take_the_whole_wave_path(dev, shape):

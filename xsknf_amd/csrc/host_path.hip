@@ -223,8 +223,11 @@ int complete(xsknf_gpu_ctx *c, Slot &s) {
 
 // ---- RESIDENT: the ring --------------------------------------------------------
 
-constexpr uint64_t kResIdleTicks = 500000;      // 5 ms without a batch (100 MHz wall clock)
-constexpr uint64_t kResLifeTicks = 100000000;   // 1 s
+// Short lives: a launch on another stream that shares the resident kernel's
+// hardware queue waits behind it, so the kernel leaves every few ms (a relaunch
+// costs one launch, ~0.5 % of a busy ring's time) and after 1 ms without a batch.
+constexpr uint64_t kResIdleTicks = 100000;      // 1 ms without a batch (100 MHz wall clock)
+constexpr uint64_t kResLifeTicks = 400000;      // 4 ms
 
 // Launch the resident kernel unless one is running.  Block b starts at entry
 // b's batch if that is published and not done, else at the entry's next
