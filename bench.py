@@ -93,6 +93,8 @@ def parse():
                    help="N > 1: skip the distribution of a root-resident global IMIX batch (SURVEY 8(e) "
                         "collective 1, reported as `root_scatter`; timed by default when N > 1)")
     p.add_argument("--no-probes", action="store_true", help="skip the read / step-floor probes")
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the RFC receive-side check of the primary and config4 outputs (rfc_check)")
     p.add_argument("--rotate", type=int, default=0,
                    help="batches the steps cycle through (0 = enough to exceed --rotate-bytes)")
     p.add_argument("--rotate-bytes", type=int, default=1 << 30)
@@ -383,11 +385,14 @@ def time_workload(name, args, world, rank, dev, seed, primary):
 
     vh = verdicts[:n].cpu().numpy()
     counters = allreduce_sum_i64([n, bytes_len, int((vh == -1).sum()), int((vh >= 0).sum())], world)
+    # batch 0 has just had a -i 1 pass (NIC workloads: every pass is -i 1)
+    rfc = rfc_verify(umem, descs, n, world) if (primary or name == "config4") and not args.no_verify else None
     shape = {"lanes_per_frame": cfg.lanes_per_frame, "chunks_per_lane": cfg.chunks_per_lane,
              "items_in_flight": cfg.frames_per_group, "window_chunks": cfg.window_chunks & 15,
              "tile_pool": bool(cfg.kernel == 1 and cfg.window_chunks & 32),
              "frame_len_max": hint, "frame_len_mean": mean}
     return dict(name=name, desc=desc, n=n, K=K, lens=lens, bytes_len=bytes_len, step_ms=step_ms, stores=stores,
+                rfc=rfc,
                 shape=shape,
                 step_ms_max=step_ms_max,
                 sum_ms=k_ms, single_kernel=single_kernel, family=family, wall_max=wall_max, counters=counters,
@@ -440,6 +445,7 @@ def root_scatter_leg(args, world, rank, dev):
     step_s = allreduce_max(e0.elapsed_time(e1) / reps / 1e3, world)
     dl = ld.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1)
     vh = v.cpu().numpy()
+    rfc = None if args.no_verify else rfc_verify(lu, ld, n_local, world)   # the last pass was -i 1
     moved = (b1 - b0 + 16 * n_local) if rank != 0 else 0
     tot = allreduce_sum_i64([n_local, int(dl["len"].astype(np.int64).sum()), moved,
                              int((vh == -1).sum()), int((vh >= 0).sum())], world)
@@ -451,7 +457,26 @@ def root_scatter_leg(args, world, rank, dev):
             "checksum_step_us_max": round(step_s * 1e6, 2),
             "gbs_checksummed": round(tot[1] / step_s / 1e9, 1),
             "verdicts": {"drop": tot[3], "forward": tot[4]},
+            "rfc_check": rfc,
             "layout": "IMIX 64/570/1500 (7:4:1) packed, unaligned-mode descriptors; shards by bytes"}
+
+
+def rfc_verify(umem, descs, n, world):
+    """Every well-formed frame's written check passes the RFC 768 / 1071
+    receive-side verification (tests/rfc1071.py, written from the RFC, no
+    restatement of the checksummer): V = 0xFFFF, or 0x0001 where the reference's
+    single fold (checksummer_user.c:105-106) drops a carry.  A size-independent
+    property of the full batch after its last -i 1 pass; all-reduced over the
+    ranks: [frames checked, violations, carry-loss frames]."""
+    from tests import rfc1071
+    d = descs[:n].cpu().numpy().view(frames.DESC_DTYPE).reshape(-1)
+    offs = ((d["addr"] & np.uint64((1 << 48) - 1)) + (d["addr"] >> np.uint64(48))).astype(np.int64)
+    idx, V = rfc1071.verify(umem, offs, d["len"].astype(np.int64))
+    c = allreduce_sum_i64([int(idx.size), int(((V != 0xFFFF) & (V != 0x0001)).sum()), int((V == 0x0001).sum())],
+                          world)
+    return {"frames_checked": c[0], "violations": c[1], "carry_loss_frames": c[2],
+            "property": "RFC 768/1071 receive-side sum of every well-formed frame = 0xFFFF (0x0001 where the "
+                        "single fold drops a carry), after the workload's last -i 1 pass"}
 
 
 # ---- CPU baseline, probes, traffic -----------------------------------------------
@@ -600,6 +625,8 @@ def step_summary(r, steps):
     out["kernel"] = f"{r['family']} ({r['stores']})"
     out["launch_shape"] = r["shape"]
     out["traffic"] = traffic_for(r["name"])
+    if r.get("rfc") is not None:
+        out["rfc_check"] = r["rfc"]
     return out
 
 
@@ -682,6 +709,7 @@ def main():
                        "parallelism": f"shard{world} (independent frames, no exchange)"},
             "roofline": roof, "cpu_baseline": cpu, "secondary": sec,
             "verdicts": {"drop": n_drop, "forward": n_fwd},
+            "rfc_check": prim["rfc"],
         }
         if rehearsal:
             out["config"]["rehearsal"] = rehearsal
