@@ -89,6 +89,9 @@ def parse():
                    help="threads for the all-cores CPU leg (-1 = the process's CPUs, at most 16; 0 = skip)")
     p.add_argument("--min-warmup-s", type=float, default=0.1,
                    help="keep warming up (untimed) until this much time has passed")
+    p.add_argument("--primary-warmup-s", type=float, default=1.0,
+                   help="the same for the primary workload (1500 B on one box: 278.4 us after 3 s of warmup "
+                        "twice, 278.4 and 281.5 after 0.1 s)")
     p.add_argument("--no-root-scatter", action="store_true",
                    help="N > 1: skip the distribution of a root-resident global IMIX batch (SURVEY 8(e) "
                         "collective 1, reported as `root_scatter`; timed by default when N > 1)")
@@ -303,7 +306,8 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    while time.perf_counter() - t_w < args.min_warmup_s:
+    warm_s = max(args.min_warmup_s, args.primary_warmup_s if primary else 0.0)
+    while time.perf_counter() - t_w < warm_s:
         for _ in range(10):
             step()
         torch.cuda.synchronize()
