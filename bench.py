@@ -704,6 +704,7 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s checksummed",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "min_warmup_s": args.min_warmup_s,
+            "primary_warmup_s": args.primary_warmup_s,
             "ms_per_step": round(step_s * 1e3, 4), "kernel_steps": args.kernel_steps,
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u16 words summed in u32", "data": "synthetic",
