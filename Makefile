@@ -41,7 +41,11 @@ PROBE := tools/build/hbm_probe
 PROBELIB := tools/build/libhbm_probe.so
 HOOKBENCH := tools/build/hook_bench
 CTXLAT := tools/build/ctx_latency
-tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH) $(CTXLAT)
+BARPROBE := tools/build/bar_probe
+tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH) $(CTXLAT) $(BARPROBE)
+$(BARPROBE): tools/bar_probe.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 $(PROBE): tools/hbm_probe.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Wno-inline-asm -o $@ $<
