@@ -2096,9 +2096,10 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
 
 // ---- the resident worker (checksummer_internal.h) ------------------------------
 //
-// Block b owns ring entry b: its first lane polls the entry in host memory for
-// the next sequence number that maps to it (system-scope acquire loads: vector
-// loads that bypass the caches), the block checksums the batch (the register
+// Block b owns ring entry b: its first lane polls the entry's header (in host
+// memory, or in device memory the host writes through the BAR) for the next
+// sequence number that maps to it (system-scope acquire loads: vector loads
+// that bypass the caches), the block checksums the batch (the register
 // kernel's tiles, 8 lanes x 12 chunks per frame: a frame of up to 1536 B in one
 // pass, the whole batch in one or two rounds of PCIe reads), and the first
 // lane stores `done` to host memory (system-scope release).  A block leaves
@@ -2108,12 +2109,16 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
 // then starts at its entry's first batch not done).  Every wave reaches an
 // exit: the poll loops are bounded by the clock, and a batch is a bounded loop.
 constexpr int kResLpf = 8, kResNch = 12, kResSpt = 2;
+#ifndef XSKNF_RES_FENCE   // A/B timing only: 0 drops the system-scope cache maintenance (unsafe)
+#define XSKNF_RES_FENCE 1
+#endif
 
 __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
   __shared__ uint64_t cmd;
   __shared__ uint32_t hdr[3];
   const uint32_t b = blockIdx.x;
-  ResSlot &e = ra.slots[b];
+  ResIn &e = ra.in[b];
+  ResOut &o = ra.out[b];
   const uint64_t t0 = wall_clock64();
   uint64_t last = t0;
   for (uint64_t seq = ra.start[b];; seq += kResSlots) {
@@ -2136,7 +2141,7 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
         }
         if (c != kResQuit) {
           // the host's writes of this batch (header, descriptors, frames), seen from this CU
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
+          if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
           hdr[0] = __hip_atomic_load(&e.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           hdr[1] = static_cast<uint32_t>(__hip_atomic_load(&e.fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
           hdr[2] = __hip_atomic_load(&e.payload_mult, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2157,8 +2162,8 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
       if (a.n) group_tiles<kResLpf, kResNch, kResSpt>(a, 0, 1);
       __syncthreads();   // the block's stores are done (workgroup release / acquire)
       if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
-        __hip_atomic_store(&e.done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
+        __hip_atomic_store(&o.done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         last = wall_clock64();
       }
     }

@@ -63,14 +63,19 @@ constexpr uint32_t kResSlots = 8;        // ring entries = blocks of the residen
 constexpr uint32_t kResFrames = 256;     // frames per entry (larger batches take the launch path)
 constexpr uint64_t kResQuit = ~0ull;
 
-struct alignas(64) ResSlot {   // host memory, coherent and mapped
-  uint64_t seq;                // host -> device: the entry's batch (release), ring sequence numbers from 1
+struct alignas(64) ResIn {     // host -> device: the entry's header.  Coherent mapped host memory,
+                               // or (large-BAR devices) fine-grained device memory the host writes
+                               // through the BAR, so the polls and header reads stay on the device
+  uint64_t seq;                // the entry's batch (release), ring sequence numbers from 1
   uint32_t n;                  // written before seq
   int32_t fwd;                 // forward verdict (prepare())
   uint32_t payload_mult;
-  uint32_t pad1;
-  uint64_t done;               // device -> host: seq once the batch is complete (release)
-  uint32_t pad[8];
+  uint32_t pad[11];
+};
+
+struct alignas(64) ResOut {    // device -> host: host memory, coherent and mapped
+  uint64_t done;               // seq once the batch is complete (release)
+  uint64_t pad[7];
 };
 
 struct alignas(64) ResCtl {    // host memory, coherent and mapped
@@ -84,8 +89,9 @@ struct ResDev {                // device memory, zeroed by the host before each 
 
 struct ResArgs {
   KernelArgs base;             // the mapped UMEM and the in-line store modes; n / fwd / mult per batch
-  ResSlot *slots;              // device views of the host arrays
+  ResIn *in;                   // device views: headers and descriptors (beside ResIn) ...
   xsknf_gpu_desc *descs;       // kResSlots x kResFrames
+  ResOut *out;                 // ... completion flags and verdicts (host memory)
   int32_t *verdicts;           // kResSlots x kResFrames
   ResCtl *ctl;
   ResDev *dev;

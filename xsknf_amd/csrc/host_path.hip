@@ -56,6 +56,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <immintrin.h>
 #include <algorithm>
 #include <atomic>
 #include <new>
@@ -121,8 +122,10 @@ struct xsknf_gpu_ctx {
   uint64_t seq = 0;                         // pieces submitted
   xsknf_gpu_ctx_stats stats = {};
   // RESIDENT: the ring (host memory, coherent, mapped) and the kernel's state
-  xsknf_gpu::ResSlot *rslots = nullptr;
+  xsknf_gpu::ResIn *rin = nullptr;          // headers + descriptors: host memory, or device memory (BAR)
   xsknf_gpu_desc *rdescs = nullptr;
+  bool rbar = false;                        // rin / rdescs are device memory written through the BAR
+  xsknf_gpu::ResOut *rout = nullptr;        // completion flags + verdicts: host memory
   int32_t *rverd = nullptr;
   xsknf_gpu::ResCtl *rctl = nullptr;
   xsknf_gpu::ResArgs ra = {};               // device views, filled at creation / registration
@@ -180,8 +183,8 @@ void release(xsknf_gpu_ctx *c) {
   if (c->path == XSKNF_GPU_PATH_RESIDENT && c->device >= 0 && c->device < 64) g_resident[c->device].fetch_sub(1);
   if (c->rdone) (void)hipEventDestroy(c->rdone);
   if (c->rstream) (void)hipStreamDestroy(c->rstream);
-  if (c->rslots) (void)hipHostFree(c->rslots);
-  if (c->rdescs) (void)hipHostFree(c->rdescs);
+  if (c->rin) (void)(c->rbar ? hipFree(c->rin) : hipHostFree(c->rin));   // rdescs lies in the same block
+  if (c->rout) (void)hipHostFree(c->rout);
   if (c->rverd) (void)hipHostFree(c->rverd);
   if (c->rctl) (void)hipHostFree(c->rctl);
   if (c->rdev) (void)hipFree(c->rdev);
@@ -244,7 +247,7 @@ int ring_launch(xsknf_gpu_ctx *c) {
     const RingEntry &e = c->ring[b];
     if (e.rseq == 0)
       ra.start[b] = b ? b : kResSlots;   // the entry's first sequence number (they start at 1)
-    else if (__atomic_load_n(&c->rslots[b].done, __ATOMIC_ACQUIRE) == e.rseq)
+    else if (__atomic_load_n(&c->rout[b].done, __ATOMIC_ACQUIRE) == e.rseq)
       ra.start[b] = e.rseq + kResSlots;
     else
       ra.start[b] = e.rseq;
@@ -270,7 +273,7 @@ int ring_launch(xsknf_gpu_ctx *c) {
 int ring_complete(xsknf_gpu_ctx *c, RingEntry &r) {
   using namespace xsknf_gpu;
   if (!r.busy) return 0;
-  const xsknf_gpu::ResSlot &h = c->rslots[r.rseq % kResSlots];
+  const xsknf_gpu::ResOut &h = c->rout[r.rseq % kResSlots];
   double t0 = 0;
   for (uint32_t spin = 1; __atomic_load_n(&h.done, __ATOMIC_ACQUIRE) != r.rseq; ++spin) {
     __builtin_ia32_pause();
@@ -313,11 +316,15 @@ int ring_submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint3
   rc = ring_complete(c, e);   // the entry's previous batch
   if (rc) return rc;
   memcpy(c->rdescs + static_cast<size_t>(k) * kResFrames, descs, sizeof(xsknf_gpu_desc) * n);
-  ResSlot &h = c->rslots[k];
+  ResIn &h = c->rin[k];
   h.n = n;
   h.fwd = a.fwd_verdict;
   h.payload_mult = a.payload_mult;
+  // a BAR mapping is write-combining: the descriptors and header must be out
+  // before the doorbell, and the doorbell out of the buffer
+  if (c->rbar) _mm_sfence();
   __atomic_store_n(&h.seq, r, __ATOMIC_RELEASE);
+  if (c->rbar) _mm_sfence();
   c->rseq = r;
   c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
   e.busy = true;
@@ -545,8 +552,23 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
   if (e == hipSuccess && path == XSKNF_GPU_PATH_RESIDENT) {
     using namespace xsknf_gpu;
     const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-    e = hipHostMalloc(&c->rslots, sizeof(ResSlot) * kResSlots, fl);
-    if (e == hipSuccess) e = hipHostMalloc(&c->rdescs, sizeof(xsknf_gpu_desc) * kResSlots * kResFrames, fl);
+    // headers and descriptors in one block: ResIn[kResSlots], then the descriptors
+    const size_t in_bytes = sizeof(ResIn) * kResSlots + sizeof(xsknf_gpu_desc) * kResSlots * kResFrames;
+    int large_bar = 0;
+    const char *bar_env = getenv("XSKNF_RESIDENT_BAR");   // 0: keep the ring in host memory (A/B)
+    if ((!bar_env || atoi(bar_env) != 0) &&
+        hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) == hipSuccess && large_bar) {
+      void *p = nullptr;
+      if (hipExtMallocWithFlags(&p, in_bytes, hipDeviceMallocFinegrained) == hipSuccess) {
+        c->rin = static_cast<ResIn *>(p);
+        c->rbar = true;
+      } else {
+        (void)hipGetLastError();
+      }
+    }
+    if (!c->rin) e = hipHostMalloc(&c->rin, in_bytes, fl);
+    if (e == hipSuccess) c->rdescs = reinterpret_cast<xsknf_gpu_desc *>(c->rin + kResSlots);
+    if (e == hipSuccess) e = hipHostMalloc(&c->rout, sizeof(ResOut) * kResSlots, fl);
     if (e == hipSuccess) e = hipHostMalloc(&c->rverd, sizeof(int32_t) * kResSlots * kResFrames, fl);
     if (e == hipSuccess) e = hipHostMalloc(&c->rctl, sizeof(ResCtl), fl);
     if (e == hipSuccess) e = hipMalloc(&c->rdev, sizeof(ResDev));
@@ -554,11 +576,21 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->rdone, hipEventDisableTiming);
     if (e == hipSuccess) {
-      memset(c->rslots, 0, sizeof(ResSlot) * kResSlots);
+      for (uint32_t k = 0; k < kResSlots; ++k) {   // (host stores: the BAR mapping is the same address)
+        c->rin[k].seq = 0;
+        c->rout[k].done = 0;
+      }
+      if (c->rbar) _mm_sfence();
       memset(c->rctl, 0, sizeof(ResCtl));
-      e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.slots), c->rslots, 0);
+      if (c->rbar) {
+        c->ra.in = c->rin;
+        c->ra.descs = c->rdescs;
+      } else {
+        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.in), c->rin, 0);
+        if (e == hipSuccess) c->ra.descs = reinterpret_cast<xsknf_gpu_desc *>(c->ra.in + kResSlots);
+      }
     }
-    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.descs), c->rdescs, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.out), c->rout, 0);
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.verdicts), c->rverd, 0);
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.ctl), c->rctl, 0);
     c->ra.dev = c->rdev;
