@@ -174,7 +174,7 @@ class HostPath:
     array (the worker's mmap), pinned while registered; `process_batch` takes
     host descriptors (DESC_DTYPE) and returns host int32 verdicts, with the check
     bytes rewritten in `umem`.  path: "zerocopy", "staged" or "resident" (zero-copy,
-    batches of <= 1024 frames through the resident kernel's ring: no launch)."""
+    every batch through the resident kernel's ring: no launch per batch)."""
 
     PATHS = {"zerocopy": _lib.PATH_ZEROCOPY, "staged": _lib.PATH_STAGED, "resident": _lib.PATH_RESIDENT}
 

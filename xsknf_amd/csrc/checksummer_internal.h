@@ -60,7 +60,7 @@ void set_error_text(const char *text);
 // per batch, and up to kResSlots batches in flight at once: the ~10 us launch
 // and completion round trip of a small batch becomes a doorbell and a flag.
 constexpr uint32_t kResSlots = 8;        // ring entries = blocks of the resident kernel
-constexpr uint32_t kResFrames = 256;     // frames per entry (larger batches take the launch path)
+constexpr uint32_t kResFrames = 256;     // frames per entry (a larger batch takes several)
 constexpr uint64_t kResQuit = ~0ull;
 
 struct alignas(64) ResIn {     // host -> device: the entry's header.  Coherent mapped host memory,

@@ -40,16 +40,19 @@
 //   share it (their frames are distinct, and a run's gap bytes are the host's
 //   own bytes).
 //
-// RESIDENT: ZEROCOPY, but a batch of at most kResFrames frames does not launch
-//   a kernel: a resident kernel (checksummer.hip resident_kernel) takes it from
-//   a ring in host memory (one 4-wave block per entry, so up to eight batches
-//   are processed at once).  submit() writes the descriptors and the entry's
+// RESIDENT: ZEROCOPY, but no batch launches a kernel: a resident kernel
+//   (checksummer.hip resident_kernel) takes the batches from a ring, in entries
+//   of up to kResFrames frames, one 4-wave block per entry, so several batches
+//   (or the pieces of a larger one) are processed at once.  The ring's headers
+//   and descriptors sit in device memory the host writes through the BAR
+//   (large-BAR devices) or in mapped host memory; completion flags and
+//   verdicts in host memory.  submit() writes the descriptors and the entry's
 //   header and publishes its sequence number; wait() spins on the entry's
 //   `done`.  The kernel exits when idle or old (or at destroy) and submit() /
-//   wait() relaunch it from the first entry not done, so a worker pays a
-//   launch only after a pause in its traffic.  A batch larger than an entry
-//   takes several entries (blocks) at once; no batch takes the launch path,
-//   whose kernels could queue behind the resident one (resident_acquire).
+//   wait() relaunch it from each entry's first batch not done, so a worker
+//   pays a launch only after a pause in its traffic.  No batch takes the
+//   launch path, whose kernels could queue behind the resident one
+//   (resident_acquire).
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
