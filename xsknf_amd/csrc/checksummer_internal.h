@@ -59,8 +59,12 @@ void set_error_text(const char *text);
 // (the register kernel's tiles: group_tiles) and publishes `done`.  No launch
 // per batch, and up to kResSlots batches in flight at once: the ~10 us launch
 // and completion round trip of a small batch becomes a doorbell and a flag.
-constexpr uint32_t kResSlots = 8;        // ring entries = blocks of the resident kernel
-constexpr uint32_t kResFrames = 256;     // frames per entry (a larger batch takes several)
+#ifndef XSKNF_RES_SLOTS   // (A/B: tools/ab_resring.sh)
+#define XSKNF_RES_SLOTS 8
+#define XSKNF_RES_FRAMES 256
+#endif
+constexpr uint32_t kResSlots = XSKNF_RES_SLOTS;     // ring entries = blocks of the resident kernel
+constexpr uint32_t kResFrames = XSKNF_RES_FRAMES;   // frames per entry (a larger batch takes several)
 constexpr uint64_t kResQuit = ~0ull;
 
 struct alignas(64) ResIn {     // host -> device: the entry's header.  Coherent mapped host memory,
