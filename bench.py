@@ -213,16 +213,30 @@ def rotation(lens: np.ndarray, args) -> int:
     return int(min(16, max(1, -(-args.rotate_bytes // max(1, touched)))))
 
 
+def batches_and_streams(name, lens_in, args):
+    """(K rotated batches, S launch streams).  With S > 1, steps in flight
+    together own distinct batches and every visit of a batch goes to the same
+    stream (K a multiple of S), so the visits of a batch stay ordered.  NIC
+    workloads time each step by its own events: one stream."""
+    K = rotation(lens_in, args)
+    S = args.streams if name not in NIC else 1
+    if S > 1:
+        K = -(-max(K, S) // S) * S
+    return K, S
+
+
+def iterations_of_step(it: int, K: int) -> int:
+    """csum_iterations of step `it` of a base workload: each visit of a batch
+    (step it touches batch it % K) alternates 1 and 2, so every check the
+    previous visit wrote changes again."""
+    return 1 + ((it // K) & 1)
+
+
 def time_workload(name, args, world, rank, dev, seed, primary):
     length, layout, chunk, desc = WORKLOADS[name]
     lens_in, span = workload_lengths(name, args, world, rank)
     n = int(lens_in.shape[0])
-    K = rotation(lens_in, args)
-    S = args.streams if name not in NIC else 1
-    if S > 1:
-        # steps in flight together own distinct batches, and every visit of a
-        # batch goes to the same stream (K a multiple of S), so visits stay ordered
-        K = -(-max(K, S) // S) * S
+    K, S = batches_and_streams(name, lens_in, args)
     # K batches of the same shape in one UMEM (batch j = frames [j*n, (j+1)*n)),
     # step i processes batch i % K
     umem, descs, lens = frames.device_batch(n * K, np.tile(lens_in, K), layout=layout, chunk=chunk or frames.CHUNK,
@@ -289,7 +303,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
 
     def step():
         j = it[0] % K
-        c = cs_alt if (not nic and (it[0] // K) & 1) else cs
+        c = cs_alt if (not nic and iterations_of_step(it[0], K) == 2) else cs
         if nic:
             evs[it[0] % len(evs)][0].record(stream)
         c.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[j], n, v_ptrs[j], 0, streams[it[0] % S].cuda_stream)
