@@ -33,9 +33,14 @@ import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
+# pageable host copies through HIP's own staging buffers, not by locking the
+# caller's pages (the runtime path behind the GPU suite's faults);
+# before the first HIP call
+os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", "1048576")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -8,6 +8,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# Copies between the GPU and PAGEABLE host memory (tensor.cpu(), .to(dev) from
+# numpy) go through HIP's own pinned staging buffers, never through HIP's
+# "pinned resource" path, which locks the caller's pageable pages for the copy
+# engine.  The four unexplained illegal-address faults of the GPU suite (rounds
+# 2-3) were writes of that path to a READ-ONLY mapped page at a host-heap address
+# (the 2.4 MB destination of a .cpu() right after two clean synchronizes), each in
+# the test after the one that locks 48 short-lived pageable buffers
+# (test_concurrent_streams) -- DESIGN 3.  Set before any HIP call, for this
+# process and every process it starts.
+os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", "1048576")
+
 # Multi-process GPU tests (ranks, the NF binary, bench.py --gpus 2) start their
 # processes from a forkserver that is launched HERE, at collection time, before
 # any test initialises the GPU: a process that has initialised the GPU must
