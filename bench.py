@@ -431,12 +431,14 @@ def root_scatter_leg(args, world, rank, dev):
     excludes the distribution, and in the reference frames arrive per NIC queue."""
     from xsknf_amd.shard import scatter_from_root
     n_total = args.frames * world
-    umem = descs = ranges = None
+    umem = descs = ranges = ref = None
     if rank == 0:
         umem, dt, lens = frames.device_batch(n_total, "imix", layout="unaligned", seed=frames.SEED, device=dev)
         descs = dt.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1)
         ranges = shard_by_bytes(lens, world)
-        del dt
+        # the single-GPU answer the shards are checked against: the whole batch
+        # through one Checksummer on rank 0, after the timed region
+        ref = (umem.clone(), dt)
     cdev = coll_device()
     if cdev == "cpu" and umem is not None:     # gloo rehearsal: host tensors
         umem = umem.cpu()
@@ -470,10 +472,23 @@ def root_scatter_leg(args, world, rank, dev):
     vh = v.cpu().numpy()
     rfc = None if args.no_verify else rfc_verify(lu, ld, n_local, world)   # the last pass was -i 1
     moved = (b1 - b0 + 16 * n_local) if rank != 0 else 0
+    fp = check_fingerprint(lu, ld, b0)
     tot = allreduce_sum_i64([n_local, int(dl["len"].astype(np.int64).sum()), moved,
-                             int((vh == -1).sum()), int((vh >= 0).sum())], world)
+                             int((vh == -1).sum()), int((vh >= 0).sum())] + fp, world)
     if rank == 0 and tot[0] != n_total:
         raise RuntimeError(f"root scatter: {tot[0]} frames arrived of {n_total}")
+    single = None
+    if rank == 0:
+        ru, rd = ref
+        rv = css[0].process_batch(ru, rd).cpu().numpy()
+        rfp = check_fingerprint(ru, rd, 0)
+        sharded = {"checks_sum": tot[5], "checks_weighted": tot[6], "drop": tot[3], "forward": tot[4]}
+        whole = {"checks_sum": rfp[0], "checks_weighted": rfp[1],
+                 "drop": int((rv == -1).sum()), "forward": int((rv >= 0).sum())}
+        single = {"match": sharded == whole, "sharded": sharded, "single_gpu": whole,
+                  "fingerprint": "sum of every frame's written check, and the same weighted by its "
+                                 "global UMEM offset mod 65521 + 1; verdict counts"}
+        del ref, ru, rd
     return {"frames_total": tot[0], "frame_bytes_total": tot[1], "bytes_moved": tot[2],
             "scatter_ms": round(t_move * 1e3, 3),
             "scatter_GBps": round(tot[2] / t_move / 1e9, 1) if t_move > 0 else None,
@@ -481,7 +496,23 @@ def root_scatter_leg(args, world, rank, dev):
             "gbs_checksummed": round(tot[1] / step_s / 1e9, 1),
             "verdicts": {"drop": tot[3], "forward": tot[4]},
             "rfc_check": rfc,
+            "vs_single_gpu": single,
             "layout": "IMIX 64/570/1500 (7:4:1) packed, unaligned-mode descriptors; shards by bytes"}
+
+
+def check_fingerprint(umem, descs, base):
+    """[sum of the written checks, the same weighted by (global offset mod 65521) + 1]
+    over the well-formed-length frames of one batch (device tensors; `base` =
+    the batch's offset in the global UMEM), so that a sharded run can be held
+    against the single-GPU run of the whole batch."""
+    d = descs.view(torch.int64).reshape(-1, 2)
+    addr = d[:, 0]
+    off = (addr & ((1 << 48) - 1)) + (addr >> 48)
+    ok = (d[:, 1] & 0xFFFFFFFF) >= 42
+    off = off[ok]
+    c = umem[off + 40].to(torch.int64) | (umem[off + 41].to(torch.int64) << 8)
+    w = (off + base) % 65521 + 1
+    return [int(c.sum()), int((c * w).sum())]
 
 
 def rfc_verify(umem, descs, n, world):

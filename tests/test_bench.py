@@ -52,3 +52,34 @@ def test_nic_workloads_time_one_stream_and_mirror_their_base():
     assert bench.batches_and_streams("1500-nic", np.full(16, 1500, np.uint32), a)[1] == 1
     for nic, base in bench.NIC.items():
         assert bench.WORKLOADS[nic][:3] == bench.WORKLOADS[base][:3]
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_check_fingerprint_of_shards_adds_up_to_the_whole(world):
+    """--root-scatter holds the shards' all-reduced fingerprint against rank 0's
+    single-GPU pass over the whole batch: with each shard's rebased descriptors
+    and its span start as base, the shards' fingerprints sum to the whole's, and
+    moving one check byte or swapping two frames' checks changes it."""
+    import torch
+    from xsknf_amd import frames
+    from xsknf_amd.shard import rebase_descs, shard_by_bytes, shard_spans
+    b = frames.unaligned_batch(3000, "imix", seed=51)
+    umem = torch.from_numpy(b.umem.copy())
+    whole_d = torch.from_numpy(b.descs.view(np.int64).reshape(-1, 2).copy())
+    whole = bench.check_fingerprint(umem, whole_d, 0)
+    ranges = shard_by_bytes(b.descs["len"], world)
+    spans = shard_spans(b.descs, ranges, umem.numel())
+    tot = [0, 0]
+    for (lo, hi), (s0, s1) in zip(ranges, spans):
+        d = torch.from_numpy(rebase_descs(b.descs[lo:hi], s0, umem.numel()).view(np.int64).reshape(-1, 2).copy())
+        f = bench.check_fingerprint(umem[s0:s1], d, s0)
+        tot = [tot[0] + f[0], tot[1] + f[1]]
+    assert tot == whole
+    offs = (b.descs["addr"] & ((1 << 48) - 1)) + (b.descs["addr"] >> 48)
+    a, c = int(offs[10]) + 40, int(offs[20]) + 40
+    if umem[a] == umem[c] and umem[a + 1] == umem[c + 1]:
+        umem[a] ^= 1
+    else:
+        umem[a], umem[c] = umem[c].clone(), umem[a].clone()
+        umem[a + 1], umem[c + 1] = umem[c + 1].clone(), umem[a + 1].clone()
+    assert bench.check_fingerprint(umem, whole_d, 0) != whole

@@ -164,3 +164,4 @@ def test_bench_gpus_n_starts_its_ranks(dev, clean_ctx):
     assert line["dist"]["ranks_seen"] == 2 and line["dist"]["world_size"] == 2
     assert line["dist"]["frames_allreduced"] == 2 * 65536
     assert line["root_scatter"]["frames_total"] == 2 * 65536
+    assert line["root_scatter"]["vs_single_gpu"]["match"] is True
