@@ -135,7 +135,7 @@ typedef int (*xsknf_batch_complete_fn)(void *user, unsigned worker_idx, void *um
 /* Batches a worker keeps in flight with the two-phase hook (1 .. XSKNF_MAX_HOOK_DEPTH,
  * default 1): after submitting a batch it completes the oldest only while more
  * than `depth` are out.  Call before xsknf_start_workers(). */
-#define XSKNF_MAX_HOOK_DEPTH 4
+#define XSKNF_MAX_HOOK_DEPTH 8
 XSKNF_API int xsknf_set_batch_depth(unsigned depth);
 
 /* Select the NF: call before xsknf_start_workers().  A batch hook (one-call or

@@ -209,10 +209,12 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            stream sharing that queue waits at most that long.
  *                            At most 3 RESIDENT contexts per device; further
  *                            ones run as ZEROCOPY.
- * One context = one worker thread.  It keeps up to five batches in flight (five slots,
- * each with its own HIP stream; XSKNF_MAX_HOOK_DEPTH batches out plus the one being
- * submitted): the copies and kernel of one overlap another's, and the host's share
- * of one overlaps the device's share of the others.
+ * One context = one worker thread.  A launched context keeps up to five batches in
+ * flight (five slots, each with its own HIP stream: four out plus the one being
+ * submitted; a deeper hook's submit waits for the oldest): the copies and kernel of
+ * one overlap another's, and the host's share of one overlaps the device's share of
+ * the others.  A RESIDENT context keeps up to eight (its ring's entries, as many as
+ * XSKNF_MAX_HOOK_DEPTH).
  * xsknf_gpu_ctx_process_batch() is synchronous: when it returns, verdicts and
  * check bytes are in host memory (a batch larger than 65536 frames runs as
  * pieces through the slots; if a piece fails to start, the pieces already

@@ -232,7 +232,7 @@ int oracle_nf_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex
  * complete would route frames on unset verdicts, and the tests see it.
  * oracle_nf_async_stats() counts submits made while another batch of the
  * worker was still recorded (the overlap the two-phase hook exists for). */
-#define ORACLE_ASYNC_DEPTH 8
+#define ORACLE_ASYNC_DEPTH 9   /* XSKNF_MAX_HOOK_DEPTH out + the one being submitted */
 #define ORACLE_ASYNC_WORKERS 64
 
 struct oracle_async_batch {

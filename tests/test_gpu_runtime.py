@@ -57,11 +57,13 @@ def test_gpu_hook_redirect_matches_oracle(frames, path, batch, two_phase):
     assert hs["batches"] >= len(frames) // batch
 
 
-@pytest.mark.parametrize("path", [_lib.PATH_ZEROCOPY, _lib.PATH_STAGED], ids=["zerocopy", "staged"])
-@pytest.mark.parametrize("depth", [2, 4])
+@pytest.mark.parametrize("path", [_lib.PATH_ZEROCOPY, _lib.PATH_STAGED, _lib.PATH_RESIDENT],
+                         ids=["zerocopy", "staged", "resident"])
+@pytest.mark.parametrize("depth", [2, 4, 8])
 def test_gpu_hook_batches_in_flight(frames, path, depth):
-    """Two-phase hook with up to `depth` batches out per worker (the context has
-    5 slots: depth 4 plus the batch being submitted)."""
+    """Two-phase hook with up to `depth` batches out per worker (a launched
+    context has 5 slots: past 4 out its submit waits for its oldest piece; the
+    resident ring has 8 entries)."""
     cfg = R.make_config(["emu0"], batch_size=64)
     got, hs, st = run_loop(cfg, {0: frames}, two_phase=True, depth=depth, path=path, iterations=3)
     assert got[0] == [b for v, b in expected(frames, iterations=3) if v != -1]

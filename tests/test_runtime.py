@@ -200,7 +200,7 @@ def async_stats(worker=0):
     return sub.value, ovl.value
 
 
-@pytest.mark.parametrize("batch,depth", [(1, 1), (64, 1), (2048, 1), (64, 3), (7, 4)])
+@pytest.mark.parametrize("batch,depth", [(1, 1), (64, 1), (2048, 1), (64, 3), (7, 4), (64, 8), (5, 8)])
 def test_async_hook_round_trip(frames, batch, depth):
     """Two-phase hook: batch k is routed only after its complete, while batch k+1
     (.. k+depth) is in flight; output identical to the per-frame path, in order."""
@@ -259,7 +259,7 @@ def test_async_hook_stop_and_restart_loses_no_frame(frames):
 def test_init_and_start_errors():
     lib = R.load()
     assert lib.xsknf_set_batch_depth(0) == -errno.EINVAL
-    assert lib.xsknf_set_batch_depth(5) == -errno.EINVAL
+    assert lib.xsknf_set_batch_depth(9) == -errno.EINVAL
     assert lib.xsknf_set_batch_processor_async(ctypes.c_void_p(1), None, None) == -errno.EINVAL
     cfg = R.make_config(["emu0"])
     cfg.working_mode = R.MODE_XDP

@@ -1,7 +1,7 @@
 // ctx_latency.c -- where a small host-path batch's time goes: CPU time inside
 // xsknf_gpu_ctx_submit (descriptor copy, launch, event) and inside
 // xsknf_gpu_ctx_wait, for batches of N frames of LEN bytes in a pinned UMEM,
-// DEPTH - 1 batches in flight behind the one being submitted (default 2; 1 =
+// DEPTH - 1 batches in flight behind the one being submitted (default 2, at most 8; 1 =
 // each batch waited for right after its submit: the round trip itself).
 //   ctx_latency LEN N ITERS [ZEROCOPY|STAGED|RESIDENT [DEPTH]]
 #include <stdint.h>
@@ -28,7 +28,7 @@ int main(int argc, char **argv)
 	                 : argc > 4 && !strcmp(argv[4], "RESIDENT") ? XSKNF_GPU_PATH_RESIDENT
 	                                                            : XSKNF_GPU_PATH_ZEROCOPY;
 	const unsigned depth = argc > 5 ? (unsigned)atoi(argv[5]) : 2;
-	if (depth < 1 || depth > 4)
+	if (depth < 1 || depth > 8)
 		return 2;
 	const unsigned nb = 64;   // distinct batches cycled through
 	const size_t chunk = 2048, size = (size_t)nb * n * chunk;
@@ -50,15 +50,15 @@ int main(int argc, char **argv)
 		return 1;
 	}
 	double t_sub = 0, t_wait = 0;
-	uint64_t tk[4] = {0, 0, 0, 0};
+	uint64_t tk[8] = {0};
 	const double t0 = now_us();
 	for (unsigned i = 0; i < iters; i++) {
 		const unsigned b = i % nb;
 		double a = now_us();
-		if (xsknf_gpu_ctx_submit(c, d + (size_t)b * n, n, 0, &o, v + (size_t)b * n, &tk[i % 4]))
+		if (xsknf_gpu_ctx_submit(c, d + (size_t)b * n, n, 0, &o, v + (size_t)b * n, &tk[i % 8]))
 			return 1;
 		double m = now_us();
-		if (i + 1 >= depth && xsknf_gpu_ctx_wait(c, tk[(i + 1 - depth) % 4]))
+		if (i + 1 >= depth && xsknf_gpu_ctx_wait(c, tk[(i + 1 - depth) % 8]))
 			return 1;
 		double e = now_us();
 		if (i >= 16) {
@@ -66,7 +66,7 @@ int main(int argc, char **argv)
 			t_wait += e - m;
 		}
 	}
-	xsknf_gpu_ctx_wait(c, tk[(iters - 1) % 4]);
+	xsknf_gpu_ctx_wait(c, tk[(iters - 1) % 8]);
 	const double total = now_us() - t0;
 	const unsigned k = iters - 16;
 	printf("{\"len\": %u, \"n\": %u, \"path\": \"%s\", \"depth\": %u, \"us_per_batch\": %.2f, "

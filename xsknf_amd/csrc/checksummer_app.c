@@ -72,8 +72,8 @@ static void usage(const char *prog)
 		"			(default: RESIDENT for batches of up to 128 frames, else ZEROCOPY).\n"
 		"  -s, --gpu-sync	One batch at a time (default: the next batch is received\n"
 		"			while the GPU checksums the last one).\n"
-		"  -d, --gpu-depth	Batches in flight per worker, 1-4 (default 2 for batches\n"
-		"			of up to 128 frames, else 1).\n"
+		"  -d, --gpu-depth	Batches in flight per worker, 1-8 (default 4 on RESIDENT,\n"
+		"			else 2 for batches of up to 128 frames, else 1).\n"
 		"  -G, --emu-gen		COUNT[:LEN] frames per emulated queue from a built-in generator.\n"
 		"\n",
 		prog);

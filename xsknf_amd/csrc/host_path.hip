@@ -11,9 +11,11 @@
 // stream, pinned descriptor / record arrays and staging buffers, so the copies
 // and kernel of one batch overlap another's, and the host's share of a batch
 // (copy plan, writing the checks) overlaps the device's share of the others.
-// Five = the runtime's deepest two-phase hook (XSKNF_MAX_HOOK_DEPTH = 4
-// batches out, include/xsknf.h) plus the batch being submitted, so a worker's
-// submit never waits for its own oldest batch.  xsknf_gpu_ctx_submit() /
+// Five = four batches out plus the one being submitted: past four out a
+// launched batch's submit is CPU-bound (launch + event, tools/ctx_depth.sh), so
+// a deeper two-phase hook (up to XSKNF_MAX_HOOK_DEPTH = 8, include/xsknf.h)
+// waits in submit for its oldest piece; the RESIDENT ring's eight entries keep
+// eight out.  xsknf_gpu_ctx_submit() /
 // _wait() expose the pipeline; the synchronous xsknf_gpu_ctx_process_batch()
 // cuts a large batch into pieces of kPiece frames and runs them through the
 // same slots.
@@ -70,7 +72,7 @@
 
 namespace {
 
-constexpr int kSlots = 5;   // pieces in flight per context: XSKNF_MAX_HOOK_DEPTH (4) batches out + the one submitted
+constexpr int kSlots = 5;   // pieces in flight per context: 4 batches out + the one submitted
 constexpr uint32_t kPiece = 65536;          // frames per slot submission of process_batch
 constexpr uint64_t kMergeGap = 256;         // frames closer than this share one DMA run
 constexpr size_t kMaxDmaRuns = 8;           // more runs than this (and no 2-D shape): mapped reads
