@@ -549,8 +549,11 @@ def test_resident_ring(dev, checks):
     """XSKNF_GPU_PATH_RESIDENT: many small batches through the resident
     kernel's ring (more in flight than it has entries, so submits wait for old
     entries), pauses longer than its idle exit (the next submit relaunches it),
-    batches of 1 and of the ring's 1024 frames, one larger batch on the launch
-    path in between; every verdict and byte equals the oracle's."""
+    batches of 1 frame up to several entries' worth (cut into 256-frame
+    pieces), runs of <= 64-frame batches (one block of an entry's group works,
+    the others fall behind the entry's numbers) followed by 256-frame batches
+    (all four work, the idle ones catching up); every verdict and byte equals
+    the oracle's."""
     import time
     from xsknf_amd import HostPath
     b = frames.unaligned_batch(12000, "imix", seed=21)
@@ -561,7 +564,7 @@ def test_resident_ring(dev, checks):
     cs = Checksummer(ChecksummerOptions(action=O.REDIRECT), num_interfaces=2, frame_len_hint=1500)
     umem = b.umem.copy()
     rng = np.random.default_rng(23)
-    sizes = [1, 64, 1024, 3000] + list(rng.integers(1, 700, size=40))
+    sizes = [1, 64, 1024, 3000] + [10] * 16 + [256] * 8 + [65] * 8 + list(rng.integers(1, 700, size=40))
     cuts = [0]
     for k in sizes:
         if cuts[-1] + k >= b.n:
@@ -573,12 +576,34 @@ def test_resident_ring(dev, checks):
         tickets = []
         for j, ((lo, hi), out) in enumerate(zip(zip(cuts[:-1], cuts[1:]), outs)):
             tickets.append(hp.submit(b.descs[lo:hi], out, ingress_ifindex=1))
-            if j in (5, 20):            # past the kernel's 5 ms idle exit
+            if j in (5, 20):            # past the kernel's 1 ms idle exit
                 hp.wait(tickets[-1])
                 time.sleep(0.03)
         hp.wait(tickets[-1])
         st = hp.stats()
     assert st["frames"] == b.n
+    assert np.array_equal(np.concatenate(outs), ov)
+    assert np.array_equal(umem, ou)
+
+
+def test_resident_ring_one_block_per_entry(dev):
+    """A resident context for batches of up to 64 frames runs one block per
+    ring entry (ResArgs::group = 1): 300 batches of 1..64 frames, more in
+    flight than the ring has entries; verdicts and bytes equal the oracle's."""
+    from xsknf_amd import HostPath
+    b = frames.unaligned_batch(10000, "imix", seed=24)
+    frames.inject_edge_cases(b, 0.05, seed=25)
+    ou, ov = run_oracle(b, iters=1, action=O.REDIRECT, nif=1)
+    cs = Checksummer(ChecksummerOptions(action=O.REDIRECT), num_interfaces=1, frame_len_hint=1500)
+    umem = b.umem.copy()
+    rng = np.random.default_rng(26)
+    cuts = [0]
+    while cuts[-1] < b.n:
+        cuts.append(min(b.n, cuts[-1] + int(rng.integers(1, 65))))
+    outs = [np.full(hi - lo, 7, dtype=np.int32) for lo, hi in zip(cuts[:-1], cuts[1:])]
+    with HostPath(cs, umem, path="resident", max_batch=64) as hp:
+        tickets = [hp.submit(b.descs[lo:hi], out) for (lo, hi), out in zip(zip(cuts[:-1], cuts[1:]), outs)]
+        hp.wait(tickets[-1])
     assert np.array_equal(np.concatenate(outs), ov)
     assert np.array_equal(umem, ou)
 

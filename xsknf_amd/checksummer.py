@@ -215,7 +215,8 @@ class HostPath:
         return verdicts
 
     def submit(self, descs, verdicts, ingress_ifindex: int = 0) -> int:
-        """Enqueue a batch (up to four in flight per context); returns its ticket.  The
+        """Enqueue a batch (a launched context keeps five pieces in flight, a
+        resident one eight; a submit past that waits for the oldest); returns its ticket.  The
         verdicts array and the batch's frames belong to the context until
         wait(ticket)."""
         if descs.dtype.itemsize != 16 or not descs.flags.c_contiguous:

@@ -2096,13 +2096,20 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
 
 // ---- the resident worker (checksummer_internal.h) ------------------------------
 //
-// Block b owns ring entry b: its first lane polls the entry's header (in host
-// memory, or in device memory the host writes through the BAR) for the next
-// sequence number that maps to it (system-scope acquire loads: vector loads
-// that bypass the caches), the block checksums the batch (the register
-// kernel's tiles, 8 lanes x 12 chunks per frame: a frame of up to 1536 B in one
-// pass, the whole batch in one or two rounds of PCIe reads), and the first
-// lane stores `done` to host memory (system-scope release).  A block leaves
+// Blocks b*kResGroup .. +kResGroup-1 own ring entry b: each one's first lane
+// polls the entry's header (in host memory, or in device memory the host
+// writes through the BAR) for the next sequence number that maps to it, which
+// carries the batch's frame count in the same word (system-scope acquire
+// loads: vector loads that bypass the caches).  The blocks deal the batch in
+// 64-frame rounds (the register kernel's tiles, 8 lanes x 12 chunks per frame:
+// a frame of up to 1536 B in one pass), so a 256-frame batch is one round of
+// PCIe reads on each of four CUs and a 64-frame batch one round on one; each
+// block with frames stores its `done` to host memory (system-scope release).
+// A context whose batches are at most 64 frames runs one block per entry
+// (ResArgs::group = 1): the idle blocks' polls cost those batches ~1 us.
+// A block without frames reads nothing but the word and moves on; it may find
+// the entry already past it (the host waits only for the blocks with frames),
+// and then takes the newer number.  A block leaves
 // when the host sets ctl->stop, after idle_ticks without a batch or after
 // life_ticks in all, and tells the others through dev->quit; a batch published
 // for a block that left waits for the host to relaunch the kernel (each block
@@ -2114,20 +2121,33 @@ constexpr int kResLpf = 8, kResNch = 12, kResSpt = 2;
 #endif
 
 __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
+  static_assert(kResBlockFrames == kWavesPerBlock * kResSpt * (kWave / kResLpf), "one round per block");
   __shared__ uint64_t cmd;
-  __shared__ uint32_t hdr[3];
-  const uint32_t b = blockIdx.x;
+  __shared__ uint32_t hdr[4];
+  // entry-minor block order: blocks are dealt to the XCDs round robin, so the
+  // entries' first blocks (the only ones a batch of <= 64 frames uses) land on
+  // eight XCDs, not on every kResGroup-th one
+  const uint32_t G = ra.group;   // blocks per entry: 1, or kResGroup (the grid is kResSlots x G)
+  const uint32_t b = blockIdx.x % kResSlots, g = blockIdx.x / kResSlots;
+  const uint32_t k = b * kResGroup + g;   // the host's index: flags and start
   ResIn &e = ra.in[b];
-  ResOut &o = ra.out[b];
+  ResOut &o = ra.out[k];
   const uint64_t t0 = wall_clock64();
   uint64_t last = t0;
-  for (uint64_t seq = ra.start[b];; seq += kResSlots) {
+  for (uint64_t seq = ra.start[k];;) {
     if (threadIdx.x == 0) {
       uint64_t c = kResQuit;
+      uint32_t n = 0;
       {
         for (;;) {
-          if (__hip_atomic_load(&e.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == seq) {
-            c = seq;
+          // a number past `seq`: the entry moved on while this block had no
+          // frames in its batches (the host waits for the blocks that do)
+          // (relaxed: the poll bypasses the caches without invalidating them;
+          // the acquire is the fence below, once a batch with frames is here)
+          const uint64_t w = __hip_atomic_load(&e.seqn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((w >> 16) >= seq) {
+            c = w >> 16;
+            n = static_cast<uint32_t>(w & 0xFFFF);
             break;
           }
           const uint64_t now = wall_clock64();
@@ -2140,11 +2160,17 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
           __builtin_amdgcn_s_sleep(2);
         }
         if (c != kResQuit) {
-          // the host's writes of this batch (header, descriptors, frames), seen from this CU
-          if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
-          hdr[0] = __hip_atomic_load(&e.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          hdr[1] = static_cast<uint32_t>(__hip_atomic_load(&e.fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-          hdr[2] = __hip_atomic_load(&e.payload_mult, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          // (the header is read only by a block with frames: the host cannot
+          // rewrite it before that block's done; a block without frames skips
+          // the fence, whose cache invalidation would cost the XCD's busy blocks)
+          hdr[3] = g < res_used_blocks(n, G);
+          hdr[0] = hdr[3] ? n : 0;
+          if (hdr[3]) {
+            // the host's writes of this batch (header, descriptors, frames), seen from this CU
+            if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
+            hdr[1] = static_cast<uint32_t>(__hip_atomic_load(&e.fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+            hdr[2] = __hip_atomic_load(&e.payload_mult, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
         }
       }
       cmd = c;
@@ -2159,14 +2185,19 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
       a.n = min(hdr[0], kResFrames);
       a.fwd_verdict = static_cast<int32_t>(hdr[1]);
       a.payload_mult = hdr[2];
-      if (a.n) group_tiles<kResLpf, kResNch, kResSpt>(a, 0, 1);
+      // the group's blocks deal the batch in 64-frame rounds: block g takes
+      // frames [64 g, 64 g + 64) of a batch of up to 256
+      if (a.n) group_tiles<kResLpf, kResNch, kResSpt>(a, g, G);
       __syncthreads();   // the block's stores are done (workgroup release / acquire)
       if (threadIdx.x == 0) {
-        if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
-        __hip_atomic_store(&o.done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (hdr[3]) {
+          if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
+          __hip_atomic_store(&o.done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         last = wall_clock64();
       }
     }
+    seq = c + kResSlots;
   }
 }
 
@@ -2238,7 +2269,7 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
 }
 
 int launch_resident(const ResArgs &ra, hipStream_t stream) {
-  hipLaunchKernelGGL(resident_kernel, dim3(kResSlots), dim3(kBlock), 0, stream, ra);
+  hipLaunchKernelGGL(resident_kernel, dim3(kResSlots * ra.group), dim3(kBlock), 0, stream, ra);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_error(e, "resident_kernel launch"); return -EIO; }
   return 0;

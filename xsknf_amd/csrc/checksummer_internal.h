@@ -53,32 +53,46 @@ void set_error_text(const char *text);
 
 // ---- the resident worker (XSKNF_GPU_PATH_RESIDENT, host_path.hip) ----------
 // A kernel that stays on the device and takes small batches from a ring in
-// host memory, one 4-wave block per ring entry: the host writes a batch's
-// descriptors and header into entry seq % kResSlots and publishes seq; the
-// entry's block polls for it, checksums the batch over PCIe in the mapped UMEM
-// (the register kernel's tiles: group_tiles) and publishes `done`.  No launch
+// host memory, a group of kResGroup 4-wave blocks per ring entry: the host
+// writes a batch's descriptors and header into entry seq % kResSlots and
+// publishes seq; the entry's blocks poll for it, checksum the batch over PCIe
+// in the mapped UMEM (the register kernel's tiles, dealt over the group:
+// group_tiles) and each publishes its own `done`.  No launch
 // per batch, and up to kResSlots batches in flight at once: the ~10 us launch
 // and completion round trip of a small batch becomes a doorbell and a flag.
 #ifndef XSKNF_RES_SLOTS   // (A/B: tools/ab_resring.sh)
 #define XSKNF_RES_SLOTS 8
 #define XSKNF_RES_FRAMES 256
 #endif
-constexpr uint32_t kResSlots = XSKNF_RES_SLOTS;     // ring entries = blocks of the resident kernel
+#ifndef XSKNF_RES_GROUP   // blocks per ring entry (A/B: tools/ab_resgroup.sh)
+#define XSKNF_RES_GROUP 4
+#endif
+constexpr uint32_t kResSlots = XSKNF_RES_SLOTS;     // ring entries
 constexpr uint32_t kResFrames = XSKNF_RES_FRAMES;   // frames per entry (a larger batch takes several)
+constexpr uint32_t kResGroup = XSKNF_RES_GROUP;     // blocks per entry: the resident kernel has
+constexpr uint32_t kResBlocks = kResSlots * kResGroup;   // kResSlots x kResGroup blocks
 constexpr uint64_t kResQuit = ~0ull;
+constexpr uint32_t kResBlockFrames = 64;   // frames one block takes per round (4 waves x 16-frame tiles)
+// blocks of an entry (`group` of them) with frames of an n-frame batch: only
+// these publish done (a block without frames moves on; the host reuses the
+// entry once these have)
+inline constexpr uint32_t res_used_blocks(uint32_t n, uint32_t group) {
+  return n == 0 ? 1 : ((n + kResBlockFrames - 1) / kResBlockFrames < group
+                           ? (n + kResBlockFrames - 1) / kResBlockFrames : group);
+}
 
 struct alignas(64) ResIn {     // host -> device: the entry's header.  Coherent mapped host memory,
                                // or (large-BAR devices) fine-grained device memory the host writes
                                // through the BAR, so the polls and header reads stay on the device
-  uint64_t seq;                // the entry's batch (release), ring sequence numbers from 1
-  uint32_t n;                  // written before seq
-  int32_t fwd;                 // forward verdict (prepare())
+  uint64_t seqn;               // the entry's batch (release): ring sequence number (from 1) << 16 | frames,
+                               // one word, so a block reads the count that belongs to the number
+  int32_t fwd;                 // forward verdict (prepare()), written before seqn
   uint32_t payload_mult;
-  uint32_t pad[11];
+  uint32_t pad[12];
 };
 
-struct alignas(64) ResOut {    // device -> host: host memory, coherent and mapped
-  uint64_t done;               // seq once the batch is complete (release)
+struct alignas(64) ResOut {    // device -> host, one per block: host memory, coherent and mapped
+  uint64_t done;               // seq once the block's share of the batch is complete (release)
   uint64_t pad[7];
 };
 
@@ -95,11 +109,12 @@ struct ResArgs {
   KernelArgs base;             // the mapped UMEM and the in-line store modes; n / fwd / mult per batch
   ResIn *in;                   // device views: headers and descriptors (beside ResIn) ...
   xsknf_gpu_desc *descs;       // kResSlots x kResFrames
-  ResOut *out;                 // ... completion flags and verdicts (host memory)
+  ResOut *out;                 // ... completion flags (kResBlocks) and verdicts (host memory)
   int32_t *verdicts;           // kResSlots x kResFrames
   ResCtl *ctl;
   ResDev *dev;
-  uint64_t start[kResSlots];   // per entry: the first sequence number its block processes
+  uint64_t start[kResBlocks];  // per block (entry x kResGroup + g): the first sequence number it processes
+  uint32_t group;              // blocks per entry in this launch: 1 or kResGroup
   uint64_t idle_ticks;         // exit after this long without a batch (100 MHz wall clock) ...
   uint64_t life_ticks;         // ... or after this long in all; the host relaunches on demand
 };

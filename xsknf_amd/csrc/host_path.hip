@@ -248,14 +248,15 @@ int ring_launch(xsknf_gpu_ctx *c) {
     if (q != hipSuccess) return fail(q, "resident kernel");
   }
   ResArgs ra = c->ra;
-  for (uint32_t b = 0; b < kResSlots; ++b) {
+  for (uint32_t k = 0; k < kResBlocks; ++k) {
+    const uint32_t b = k / kResGroup;
     const RingEntry &e = c->ring[b];
     if (e.rseq == 0)
-      ra.start[b] = b ? b : kResSlots;   // the entry's first sequence number (they start at 1)
-    else if (__atomic_load_n(&c->rout[b].done, __ATOMIC_ACQUIRE) == e.rseq)
-      ra.start[b] = e.rseq + kResSlots;
+      ra.start[k] = b ? b : kResSlots;   // the entry's first sequence number (they start at 1)
+    else if (__atomic_load_n(&c->rout[k].done, __ATOMIC_ACQUIRE) == e.rseq)
+      ra.start[k] = e.rseq + kResSlots;
     else
-      ra.start[b] = e.rseq;
+      ra.start[k] = e.rseq;
   }
   // (the previous launch, and with it the previous copy from rinit, is complete)
   c->rinit->quit = 0;
@@ -278,9 +279,15 @@ int ring_launch(xsknf_gpu_ctx *c) {
 int ring_complete(xsknf_gpu_ctx *c, RingEntry &r) {
   using namespace xsknf_gpu;
   if (!r.busy) return 0;
-  const xsknf_gpu::ResOut &h = c->rout[r.rseq % kResSlots];
+  const xsknf_gpu::ResOut *h = c->rout + (r.rseq % kResSlots) * kResGroup;
+  const uint32_t used = res_used_blocks(r.n, c->ra.group);   // the blocks with frames publish done
+  const auto all_done = [h, &r, used] {
+    for (uint32_t g = 0; g < used; ++g)
+      if (__atomic_load_n(&h[g].done, __ATOMIC_ACQUIRE) != r.rseq) return false;
+    return true;
+  };
   double t0 = 0;
-  for (uint32_t spin = 1; __atomic_load_n(&h.done, __ATOMIC_ACQUIRE) != r.rseq; ++spin) {
+  for (uint32_t spin = 1; !all_done(); ++spin) {
     __builtin_ia32_pause();
     if ((spin & 1023) == 0) {
       timespec ts;
@@ -293,7 +300,7 @@ int ring_complete(xsknf_gpu_ctx *c, RingEntry &r) {
       }
       const hipError_t q = hipEventQuery(c->rdone);
       if (q == hipSuccess) {
-        if (__atomic_load_n(&h.done, __ATOMIC_ACQUIRE) == r.rseq) break;
+        if (all_done()) break;
         const int rc = ring_launch(c);   // it exited before this entry
         if (rc) return rc;
       } else if (q != hipErrorNotReady) {
@@ -322,13 +329,12 @@ int ring_submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint3
   if (rc) return rc;
   memcpy(c->rdescs + static_cast<size_t>(k) * kResFrames, descs, sizeof(xsknf_gpu_desc) * n);
   ResIn &h = c->rin[k];
-  h.n = n;
   h.fwd = a.fwd_verdict;
   h.payload_mult = a.payload_mult;
   // a BAR mapping is write-combining: the descriptors and header must be out
   // before the doorbell, and the doorbell out of the buffer
   if (c->rbar) _mm_sfence();
-  __atomic_store_n(&h.seq, r, __ATOMIC_RELEASE);
+  __atomic_store_n(&h.seqn, r << 16 | n, __ATOMIC_RELEASE);
   if (c->rbar) _mm_sfence();
   c->rseq = r;
   c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
@@ -573,7 +579,7 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
     }
     if (!c->rin) e = hipHostMalloc(&c->rin, in_bytes, fl);
     if (e == hipSuccess) c->rdescs = reinterpret_cast<xsknf_gpu_desc *>(c->rin + kResSlots);
-    if (e == hipSuccess) e = hipHostMalloc(&c->rout, sizeof(ResOut) * kResSlots, fl);
+    if (e == hipSuccess) e = hipHostMalloc(&c->rout, sizeof(ResOut) * kResBlocks, fl);
     if (e == hipSuccess) e = hipHostMalloc(&c->rverd, sizeof(int32_t) * kResSlots * kResFrames, fl);
     if (e == hipSuccess) e = hipHostMalloc(&c->rctl, sizeof(ResCtl), fl);
     if (e == hipSuccess) e = hipMalloc(&c->rdev, sizeof(ResDev));
@@ -581,10 +587,9 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->rdone, hipEventDisableTiming);
     if (e == hipSuccess) {
-      for (uint32_t k = 0; k < kResSlots; ++k) {   // (host stores: the BAR mapping is the same address)
-        c->rin[k].seq = 0;
-        c->rout[k].done = 0;
-      }
+      for (uint32_t k = 0; k < kResSlots; ++k)   // (host stores: the BAR mapping is the same address)
+        c->rin[k].seqn = 0;
+      for (uint32_t k = 0; k < kResBlocks; ++k) c->rout[k].done = 0;
       if (c->rbar) _mm_sfence();
       memset(c->rctl, 0, sizeof(ResCtl));
       if (c->rbar) {
@@ -599,6 +604,9 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.verdicts), c->rverd, 0);
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.ctl), c->rctl, 0);
     c->ra.dev = c->rdev;
+    // batches of up to 64 frames: one block per entry (a group's idle blocks
+    // would cost them ~1 us); larger ones: the group deals 64-frame rounds
+    c->ra.group = max_batch <= kResBlockFrames ? 1 : kResGroup;
   }
   if (e != hipSuccess) {
     const int rc = fail(e, "xsknf_gpu_ctx_create");
