@@ -200,8 +200,9 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            ring in host memory (the submit writes the
  *                            descriptors and rings a doorbell, the wait spins
  *                            on a completion flag), 8 entries of up to 256
- *                            frames, one block each, so up to 8 batches (or
- *                            pieces of a larger one) are processed at once.
+ *                            frames, one block each when max_batch <= 64,
+ *                            else four (64 frames each), so up to 8 batches
+ *                            (or pieces of a larger one) are processed at once.
  *                            For the rx loop's small batches.  The kernel leaves
  *                            after 1 ms without a batch (and after 4 ms in all)
  *                            and the next submit or wait relaunches it: it holds
