@@ -95,8 +95,12 @@ asm: $(SRCS)
 	@mkdir -p build/asm
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o $(ASM) xsknf_amd/csrc/checksummer.hip
 
+# the restatement, and (where the reference checkout exists) the reference's
+# own per-packet function compiled from its verbatim lines (oracle/_ref)
+REF ?= /root/reference
 oracle:
 	$(MAKE) -C oracle
+	if [ -d $(REF)/examples/checksummer ]; then $(MAKE) -C oracle ref REF=$(REF); fi
 
 clean:
 	rm -rf $(LIBDIR) xsknf_amd/bin build

@@ -546,33 +546,42 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(res, budget_s, threads, check=True):
-    """Oracle (the C restatement, gcc -O2 -flto) timed on host cores over a bounded
-    sample of the same workload; also checks the GPU result on that sample."""
+    """The reference's own xsknf_packet_processor() (oracle/_ref: its verbatim
+    text compiled gcc -O2 -flto, kind "reference") -- or, where that library was
+    not built, the C restatement (kind "port") -- timed on host cores in a
+    process_batch_1if-shaped loop over a bounded sample of the same workload;
+    also checks the GPU result on that sample."""
     from oracle import csum_oracle as O
+    from oracle import ref as R
 
+    kind = "reference" if R.available() else "port"
+    timer = R.time_batch if kind == "reference" else O.c_time_batch
+    process = R.process_batch if kind == "reference" else O.c_process_batch
     umem_host, descs_host, k = res["sample"]
     lens = descs_host["len"].astype(np.int64)
     work = umem_host.copy()
-    t1, v = O.c_time_batch(work, descs_host, threads=threads, reps=1)
+    t1, v = timer(work, descs_host, threads=threads, reps=1)
     reps = max(1, int(budget_s / max(t1, 1e-6)))
-    t, v = O.c_time_batch(work, descs_host, threads=threads, reps=reps)
+    t, v = timer(work, descs_host, threads=threads, reps=reps)
     gbs = lens.sum() * reps / t / 1e9
-    # checker: GPU output on the sample frames == oracle output (single pass;
-    # reprocessing is idempotent because the check is cleared before summing)
+    # checker: GPU output on the sample frames == the CPU path's output (single
+    # pass; reprocessing is idempotent because the check is cleared before summing)
     match = None
     if check:
-        O.c_process_batch(umem_host, descs_host)
+        process(umem_host, descs_host)
         hi = umem_host.shape[0]
         g_umem = res["umem"][:hi].cpu().numpy()
         g_v = res["verdicts"][:k].cpu().numpy()
         match = bool(np.array_equal(g_v, v) and np.array_equal(g_umem, umem_host))
     return {"value": round(float(gbs), 4), "unit": "GB/s checksummed", "cores": threads,
-            "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "kind": kind, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "mpps": round(k * reps / t / 1e6, 4),
             "sample": f"{k} frames of the same workload ({lens.sum() / 1e6:.1f} MB) x {reps} passes, "
                       f"{t:.1f} s, process_batch_1if-shaped loop (batch 64), 1 pinned core"
                       if threads == 1 else f"{k} frames x {reps} passes, {threads} threads",
-            "gpu_matches_oracle_on_sample": match}
+            "gpu_matches_oracle_on_sample": match,
+            "code": "oracle/_ref/libcsum_ref.so: reference checksummer_user.c:30-112 verbatim, gcc -O2 -flto"
+                    if kind == "reference" else "oracle/csum_oracle.c (restatement), gcc -O2 -flto"}
 
 
 def probes_for(res, reps=20):

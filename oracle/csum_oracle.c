@@ -19,10 +19,11 @@
  * it is an independent statement of the algorithm from the GPU kernel, which
  * uses the closed byte-parity form.
  *
- * Parity pin: the reference cannot be built in this image (its headers need
- * libbpf/libxdp, which are absent), so this restatement is pinned by the
- * known-answer vectors C1-C6 recorded in SURVEY.md Appendix C (produced from
- * the compiled reference during the survey) -- see tests/test_oracle.py.
+ * Parity pin: the reference's own xsknf_packet_processor() is compiled here
+ * from its verbatim text (oracle/ref_extract.sh + ref_harness.c ->
+ * oracle/_ref/libcsum_ref.so, `make -C oracle ref`); tests/test_ref_pin.py
+ * holds this restatement equal to it byte for byte on 20,000 randomized
+ * frames and the known answers C1-C6, and tests/golden/ is its output.
  */
 #define _GNU_SOURCE
 #include <pthread.h>

@@ -5,8 +5,8 @@ Three independent restatements of reference examples/checksummer/checksummer_use
   * `py_packet_processor` a pure-Python literal transliteration (small inputs);
   * `np_packet_processor` the closed byte-parity form in numpy,
     which is how the GPU kernel computes, but written independently of it.
-All three are cross-checked against each other and pinned by the known answers
-C1-C6 of SURVEY.md Appendix C (tests/test_oracle.py).
+All three are cross-checked against each other (tests/test_oracle.py) and pinned
+to the reference's own function compiled here (oracle/ref.py, tests/test_ref_pin.py).
 """
 from __future__ import annotations
 

@@ -1,8 +1,8 @@
 """The CPU oracle, pinned before it is trusted.
 
-Pins: the known answers C1-C6 of SURVEY.md Appendix C, which the survey produced
-from the reference's own checksummer_user.c compiled in the survey container
-(the reference cannot be rebuilt in this image: it needs libbpf/libxdp).
+Pins: the reference's own checksummer_user.c:30-112, compiled here from its
+verbatim text (oracle/_ref, tests/test_ref_pin.py), and the known answers C1-C6
+of SURVEY.md Appendix C, which that library reproduces.
 Cross-checks: three independent restatements (C literal loop, Python literal
 loop, numpy closed form) must agree byte-for-byte on randomized frames covering
 every branch of checksummer_user.c:30-112.  Golden fixtures are checked in
