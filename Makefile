@@ -67,7 +67,7 @@ $(HOOKBENCH): tools/hook_bench.c $(RTLIB) $(LIB) oracle
 
 $(CTXLAT): tools/ctx_latency.c $(LIB)
 	@mkdir -p $(dir $@)
-	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ $< -L$(LIBDIR) -lxsknf_gpu \
+	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ $< -L$(LIBDIR) -lxsknf_gpu -pthread \
 		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 # A/B build: every kernel family and launch shape (tools/tune.py, tools/ab_libs.sh;

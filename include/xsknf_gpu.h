@@ -195,21 +195,29 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            the 4-byte records come back and the host writes
  *                            the 2 check bytes.  A batch of frames scattered
  *                            over the UMEM runs as ZEROCOPY instead.
- *   XSKNF_GPU_PATH_RESIDENT  ZEROCOPY without a launch per batch: a kernel
- *                            resident on the device takes the batches from a
- *                            ring in host memory (the submit writes the
+ *   XSKNF_GPU_PATH_RESIDENT  ZEROCOPY without a launch per batch: ONE kernel
+ *                            resident on each device serves every RESIDENT
+ *                            context of the process on that device (up to 64:
+ *                            XSKNF_MAX_WORKERS workers x two UMEMs).  Each
+ *                            context has its own ring (the submit writes the
  *                            descriptors and rings a doorbell, the wait spins
  *                            on a completion flag), 8 entries of up to 256
  *                            frames, one block each when max_batch <= 64,
  *                            else four (64 frames each), so up to 8 batches
- *                            (or pieces of a larger one) are processed at once.
- *                            For the rx loop's small batches.  The kernel leaves
- *                            after 1 ms without a batch (and after 4 ms in all)
- *                            and the next submit or wait relaunches it: it holds
- *                            a hardware queue, and work queued behind it on a
- *                            stream sharing that queue waits at most that long.
- *                            At most 3 RESIDENT contexts per device; further
- *                            ones run as ZEROCOPY.
+ *                            per context (or pieces of a larger one) are
+ *                            processed at once.  For the rx loop's small
+ *                            batches.  The kernel leaves after 1 ms without a
+ *                            batch on any ring (and after 4 ms in all) and the
+ *                            next submit or wait of any context relaunches it;
+ *                            creating or destroying a RESIDENT context stops
+ *                            and relaunches it.  It holds one hardware queue
+ *                            (GPU_MAX_HW_QUEUES is 4 by default): a process
+ *                            that also launches work of its own (ZEROCOPY /
+ *                            STAGED contexts, torch) may find a launch queued
+ *                            behind it for up to those 4 ms when its streams
+ *                            outnumber the hardware queues, so give such a
+ *                            process one path.  Creating a context returns
+ *                            -ENOSPC past 64 rings per device.
  * One context = one worker thread.  A launched context keeps up to five batches in
  * flight (five slots, each with its own HIP stream: four out plus the one being
  * submitted; a deeper hook's submit waits for the oldest): the copies and kernel of
@@ -237,6 +245,8 @@ struct xsknf_gpu_ctx_stats {
 	uint64_t frames;
 	uint64_t bytes_h2d;
 	uint64_t bytes_d2h;
+	uint64_t resident_batches;   /* ring entries the device's resident kernel completed (RESIDENT) */
+	uint64_t resident_launches;  /* launches of that kernel so far, for every context of the device */
 };
 
 XSKNF_GPU_API int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **ctx, int device, int path,

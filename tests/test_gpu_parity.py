@@ -608,33 +608,164 @@ def test_resident_ring_one_block_per_entry(dev):
     assert np.array_equal(umem, ou)
 
 
-def test_resident_contexts_past_the_limit_run_zerocopy(dev):
-    """Five RESIDENT contexts on one device at once, batches interleaved over
-    them: the first three hold resident kernels (each a hardware queue), the
-    others run as ZEROCOPY (include/xsknf_gpu.h); every context's frames come
-    out equal to the oracle's."""
+def _entries(n):
+    return -(-n // 256) if n else 0
+
+
+@pytest.mark.parametrize("n_ctx,max_batch,batch", [(8, 2000, 100), (8, 64, 50), (40, 300, 257)],
+                         ids=["8-groups-of-4", "8-groups-of-1", "40-blocks-serve-several-entries"])
+def test_resident_contexts_share_one_kernel(dev, n_ctx, max_batch, batch):
+    """Many RESIDENT contexts on one device at once -- one per worker and UMEM,
+    as the hook makes them (the reference runs up to XSKNF_MAX_WORKERS = 32
+    workers, src/xsknf.h:12, one per queue, src/xsknf.c:992) -- with batches
+    interleaved over them.  Every context stays resident: each of its batches
+    is a ring entry completed by the device's ONE resident kernel
+    (resident_batches), whose launches every context shares.  40 contexts of
+    four-block groups need more blocks than the kernel's grid may hold, so a
+    block serves several entries of its ring.  Every context's verdicts and
+    bytes equal the oracle's."""
     from xsknf_amd import HostPath
-    bs = [frames.aligned_batch(2000, "imix", chunk=2048, seed=40 + k) for k in range(5)]
+    total = 1200 if n_ctx > 8 else 2000
+    bs = [frames.aligned_batch(total, "imix", chunk=2048, seed=40 + k) for k in range(n_ctx)]
     for k, b in enumerate(bs):
         frames.inject_edge_cases(b, 0.05, seed=50 + k)
     refs = [run_oracle(b, iters=1, action=O.DROP, nif=1) for b in bs]
     cs = Checksummer(ChecksummerOptions(action=O.DROP), frame_len_hint=1500)
     umems = [b.umem.copy() for b in bs]
-    hps = [HostPath(cs, u, path="resident", max_batch=2000) for u in umems]
+    hps = []
     try:
+        for u in umems:
+            hps.append(HostPath(cs, u, path="resident", max_batch=max_batch))
         outs = [np.full(b.n, 7, dtype=np.int32) for b in bs]
         tickets = [[] for _ in bs]
-        for lo in range(0, 2000, 100):
+        for lo in range(0, total, batch):
             for k, (hp, b) in enumerate(zip(hps, bs)):
-                tickets[k].append(hp.submit(b.descs[lo:lo + 100], outs[k][lo:lo + 100]))
+                tickets[k].append(hp.submit(b.descs[lo:lo + batch], outs[k][lo:lo + batch]))
         for hp, t in zip(hps, tickets):
             hp.wait(t[-1])
+        stats = [hp.stats() for hp in hps]
+    finally:
+        for hp in hps:
+            hp.close()
+    want = sum(_entries(min(batch, total - lo)) for lo in range(0, total, batch))
+    for st in stats:
+        assert st["frames"] == total
+        assert st["resident_batches"] == want, st
+        assert st["resident_launches"] >= n_ctx      # (each context's arrival relaunches the kernel)
+    for (ou, ov), u, v in zip(refs, umems, outs):
+        assert np.array_equal(v, ov)
+        assert np.array_equal(u, ou)
+
+
+def test_resident_rings_join_and_leave_under_traffic(dev):
+    """A ring joining (a new worker's first batch) and one leaving (a context
+    destroyed) stop and relaunch the shared kernel while other contexts have
+    batches in flight: those batches are picked up by the relaunch, none is
+    processed twice (ihl 2/3 frames would show it: reprocessing them is not
+    idempotent), and every context's output equals the oracle's."""
+    from xsknf_amd import HostPath
+    bs = [frames.unaligned_batch(1500, "imix", seed=60 + k) for k in range(4)]
+    for k, b in enumerate(bs):
+        frames.inject_edge_cases(b, 0.1, seed=70 + k)
+    refs = [run_oracle(b, iters=2, action=O.REDIRECT, nif=3, ingress=1) for b in bs]
+    cs = Checksummer(ChecksummerOptions(action=O.REDIRECT, csum_iterations=2), num_interfaces=3,
+                     frame_len_hint=1500)
+    umems = [b.umem.copy() for b in bs]
+    outs = [np.full(b.n, 7, dtype=np.int32) for b in bs]
+    hp = {}
+    try:
+        hp[0] = HostPath(cs, umems[0], path="resident", max_batch=256)
+        hp[1] = HostPath(cs, umems[1], path="resident", max_batch=64)
+        t = {0: [], 1: [], 2: [], 3: []}
+        pos = {k: 0 for k in range(4)}
+
+        def feed(k, size):
+            lo = pos[k]
+            hi = min(bs[k].n, lo + size)
+            if hi > lo:
+                t[k].append(hp[k].submit(bs[k].descs[lo:hi], outs[k][lo:hi], ingress_ifindex=1))
+            pos[k] = hi
+
+        for _ in range(4):
+            feed(0, 200)
+            feed(1, 64)
+        hp[2] = HostPath(cs, umems[2], path="resident", max_batch=256)   # joins: 0 and 1 in flight
+        for _ in range(3):
+            feed(0, 200)
+            feed(1, 64)
+            feed(2, 256)
+        hp[1].wait(t[1][-1])
+        hp[1].close()                                                     # leaves: 0 and 2 in flight
+        hp[3] = HostPath(cs, umems[3], path="resident", max_batch=1500)  # joins
+        while any(pos[k] < bs[k].n for k in (0, 2, 3)):
+            for k in (0, 2, 3):
+                feed(k, 150)
+        for k in (0, 2, 3):
+            hp[k].wait(t[k][-1])
+    finally:
+        for h in hp.values():
+            h.close()
+    # context 1 left after pos[1] frames: exactly those are done
+    n1 = pos[1]
+    assert np.array_equal(outs[1][:n1], refs[1][1][:n1])
+    offs = bs[1].frame_offsets()
+    end1 = int(offs[n1 - 1] + bs[1].descs["len"][n1 - 1])
+    assert np.array_equal(umems[1][:end1], refs[1][0][:end1])
+    for k in (0, 2, 3):
+        assert np.array_equal(outs[k], refs[k][1]), k
+        assert np.array_equal(umems[k], refs[k][0]), k
+
+
+def test_resident_rings_past_the_device_limit_are_refused(dev):
+    """64 rings per device (XSKNF_MAX_WORKERS x a zero-copy and a copy-mode
+    UMEM); a 65th RESIDENT context is refused with -ENOSPC instead of running
+    some other way; the 64 keep working, bit-exact."""
+    from xsknf_amd import HostPath
+    from xsknf_amd._lib import XsknfGpuError
+    cs = Checksummer(ChecksummerOptions(action=O.REDIRECT), num_interfaces=1, frame_len_hint=1500)
+    bs = [frames.unaligned_batch(100, "imix", seed=300 + k) for k in range(64)]
+    refs = [run_oracle(b, iters=1, action=O.REDIRECT, nif=1) for b in bs]
+    umems = [b.umem.copy() for b in bs]
+    hps = []
+    try:
+        for u in umems:
+            hps.append(HostPath(cs, u, path="resident", max_batch=512))
+        extra = np.zeros(4096, dtype=np.uint8)
+        with pytest.raises(XsknfGpuError, match="rc=-28"):
+            HostPath(cs, extra, path="resident", max_batch=64)
+        outs = [hp.process_batch(b.descs) for hp, b in zip(hps, bs)]
     finally:
         for hp in hps:
             hp.close()
     for (ou, ov), u, v in zip(refs, umems, outs):
         assert np.array_equal(v, ov)
         assert np.array_equal(u, ou)
+
+
+@pytest.mark.parametrize("checks", ["zero", "nic"])
+@pytest.mark.parametrize("length", [4000, 9000])
+def test_resident_ring_long_frames(dev, length, checks):
+    """The resident kernel's register tiles cover 1536 B per pass; longer
+    frames take further passes (finish_long_frames).  Unaligned UMEM (the -u
+    layout of config 5, odd starts) with 4000 / 9000 B frames and edge cases,
+    in batches under and over 64 frames (one block and four per entry), with
+    zero checks and with the checks a NIC wrote; bit-exact."""
+    from xsknf_amd import HostPath
+    b = frames.unaligned_batch(700, length, seed=80 + length)
+    if checks == "nic":
+        frames.offload_checks_host(b)
+    frames.inject_edge_cases(b, 0.1, seed=81)
+    ou, ov = run_oracle(b, iters=1, action=O.REDIRECT, nif=1)
+    cs = Checksummer(ChecksummerOptions(action=O.REDIRECT), num_interfaces=1, frame_len_hint=length)
+    umem = b.umem.copy()
+    cuts = [0, 1, 40, 104, 360, 361, 600, 700]
+    outs = [np.full(hi - lo, 7, dtype=np.int32) for lo, hi in zip(cuts[:-1], cuts[1:])]
+    with HostPath(cs, umem, path="resident", max_batch=512) as hp:
+        tk = [hp.submit(b.descs[lo:hi], out) for (lo, hi), out in zip(zip(cuts[:-1], cuts[1:]), outs)]
+        hp.wait(tk[-1])
+        assert hp.stats()["resident_batches"] == sum(_entries(hi - lo) for lo, hi in zip(cuts[:-1], cuts[1:]))
+    assert np.array_equal(np.concatenate(outs), ov)
+    assert np.array_equal(umem, ou)
 
 
 @pytest.mark.parametrize("shape", [(16, 2, 2, 0, 1, 1, 20), (16, 3, 1, 0, 0, 1, 24), (16, 3, 2, 0, 2, 1, 20),

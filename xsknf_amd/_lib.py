@@ -76,7 +76,8 @@ class CtxStats(ctypes.Structure):
     """struct xsknf_gpu_ctx_stats (include/xsknf_gpu.h)."""
 
     _fields_ = [("batches", ctypes.c_uint64), ("frames", ctypes.c_uint64),
-                ("bytes_h2d", ctypes.c_uint64), ("bytes_d2h", ctypes.c_uint64)]
+                ("bytes_h2d", ctypes.c_uint64), ("bytes_d2h", ctypes.c_uint64),
+                ("resident_batches", ctypes.c_uint64), ("resident_launches", ctypes.c_uint64)]
 
 
 class XsknfGpuError(RuntimeError):

@@ -2096,26 +2096,46 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
 
 // ---- the resident worker (checksummer_internal.h) ------------------------------
 //
-// Blocks b*kResGroup .. +kResGroup-1 own ring entry b: each one's first lane
-// polls the entry's header (in host memory, or in device memory the host
-// writes through the BAR) for the next sequence number that maps to it, which
-// carries the batch's frame count in the same word (system-scope acquire
-// loads: vector loads that bypass the caches).  The blocks deal the batch in
+// ONE kernel per device serves every RESIDENT context's ring (ResLaunch::ring).
+// ResLaunch::block maps each block to its ring, its place g in an entry's group
+// and its first entry; a block serves entries b, b + kResSlots / E, ... of that
+// ring (E = ResArgs::entries_per_block, 1 unless the rings would need more
+// blocks than the grid may have).  Its first lane polls those entries' headers
+// (in host memory, or in device memory the host writes through the BAR) for
+// the next sequence number that maps to each, which carries the batch's frame
+// count in the same word: system-scope RELAXED loads (vector loads that bypass
+// the caches without the invalidation an acquire adds per poll), all E of them
+// issued before any is compared; the acquire is one fence once a batch with
+// frames for this block is there.  The blocks of a group deal the batch in
 // 64-frame rounds (the register kernel's tiles, 8 lanes x 12 chunks per frame:
-// a frame of up to 1536 B in one pass), so a 256-frame batch is one round of
-// PCIe reads on each of four CUs and a 64-frame batch one round on one; each
-// block with frames stores its `done` to host memory (system-scope release).
-// A context whose batches are at most 64 frames runs one block per entry
-// (ResArgs::group = 1): the idle blocks' polls cost those batches ~1 us.
-// A block without frames reads nothing but the word and moves on; it may find
-// the entry already past it (the host waits only for the blocks with frames),
-// and then takes the newer number.  A block leaves
-// when the host sets ctl->stop, after idle_ticks without a batch or after
-// life_ticks in all, and tells the others through dev->quit; a batch published
-// for a block that left waits for the host to relaunch the kernel (each block
-// then starts at its entry's first batch not done).  Every wave reaches an
-// exit: the poll loops are bounded by the clock, and a batch is a bounded loop.
+// a frame of up to 1536 B in one pass, longer ones in further passes), so a
+// 256-frame batch is one round of PCIe reads on each of four CUs and a 64-frame
+// batch one round on one; each block with frames stores its `done` to host
+// memory (system-scope release).  A ring whose batches are at most 64 frames
+// runs one block per entry (ResRing::group = 1): idle blocks' polls cost those
+// batches ~1 us.  A block without frames reads nothing but the word and moves
+// on; it may find the entry already past it (the host waits only for the
+// blocks with frames), and then takes the newer number.
+// A block leaves when the host sets ctl->stop (a ring joins or leaves), when
+// NO block has finished a batch for idle_ticks (ResLaunch::act, the clock of
+// the latest batch, kept by an atomic max), or after life_ticks in all; it
+// tells the others by setting act to kResQuit, and the last block to leave
+// reports the launch's epoch in ctl->exited.  A batch published to a kernel
+// that has left waits for the host to relaunch it (every block then starts at
+// its entries' first batch not done).  Every wave reaches an exit: the poll
+// loops are bounded by the clock, and a batch is a bounded loop.
 constexpr int kResLpf = 8, kResNch = 12, kResSpt = 2;
+
+// A wave-uniform value read from LDS, moved to scalar registers: addresses
+// built from it then use the SGPR-base forms, as with kernel arguments.
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  return static_cast<uint64_t>(uniform_u32(static_cast<uint32_t>(v >> 32))) << 32 | uniform_u32(static_cast<uint32_t>(v));
+}
+template <typename T>
+__device__ __forceinline__ T *uniform_ptr(T *p) {
+  return reinterpret_cast<T *>(uniform_u64(reinterpret_cast<uint64_t>(p)));
+}
 #ifndef XSKNF_RES_FENCE   // A/B timing only: 0 drops the system-scope cache maintenance (unsafe)
 #define XSKNF_RES_FENCE 1
 #endif
@@ -2123,54 +2143,79 @@ constexpr int kResLpf = 8, kResNch = 12, kResSpt = 2;
 __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
   static_assert(kResBlockFrames == kWavesPerBlock * kResSpt * (kWave / kResLpf), "one round per block");
   __shared__ uint64_t cmd;
-  __shared__ uint32_t hdr[4];
-  // entry-minor block order: blocks are dealt to the XCDs round robin, so the
-  // entries' first blocks (the only ones a batch of <= 64 frames uses) land on
-  // eight XCDs, not on every kResGroup-th one
-  const uint32_t G = ra.group;   // blocks per entry: 1, or kResGroup (the grid is kResSlots x G)
-  const uint32_t b = blockIdx.x % kResSlots, g = blockIdx.x / kResSlots;
-  const uint32_t k = b * kResGroup + g;   // the host's index: flags and start
-  ResIn &e = ra.in[b];
-  ResOut &o = ra.out[k];
+  __shared__ uint32_t hdr[5];
+  // the block's ring, copied to LDS once: the system-scope acquire of every
+  // batch invalidates the caches, and the ring's pointers would be re-read
+  // from memory behind it on each batch's critical path
+  __shared__ ResRing R;
+  ResLaunch *const L = ra.L;
+  const uint32_t m = L->block[blockIdx.x];
+  const uint32_t r = m >> 16, g = (m >> 8) & 0xff, b0 = m & 0xff;
+  if (threadIdx.x == 0) R = L->ring[r];
+  __syncthreads();
+  const uint32_t G = R.group;
+  const uint32_t E = ra.entries_per_block, stride = kResSlots / E;
+  // lane 0's state: the next sequence number of each entry it serves (in LDS:
+  // registers live across group_tiles would cost the kernel its second wave per SIMD)
+  __shared__ uint64_t next[kResSlots];
+  if (threadIdx.x < kResSlots)
+    next[threadIdx.x] = threadIdx.x < E ? L->start[r][(b0 + threadIdx.x * stride) * kResGroup + g] : kResQuit;
+  __syncthreads();
   const uint64_t t0 = wall_clock64();
   uint64_t last = t0;
-  for (uint64_t seq = ra.start[k];;) {
+  for (;;) {
     if (threadIdx.x == 0) {
       uint64_t c = kResQuit;
-      uint32_t n = 0;
-      {
-        for (;;) {
-          // a number past `seq`: the entry moved on while this block had no
+      uint32_t n = 0, b = b0;
+      for (bool got = false; !got;) {
+        // every word of the poll issued before any is looked at: one round
+        // trip per poll, not one per word
+        uint64_t w[kResSlots];
+#pragma unroll
+        for (uint32_t j = 0; j < kResSlots; ++j)
+          w[j] = j < E ? __hip_atomic_load(&R.in[b0 + j * stride].seqn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                       : 0;
+        const uint64_t act = __hip_atomic_load(&L->act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t stop = __hip_atomic_load(&ra.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t now = wall_clock64();
+#pragma unroll
+        for (uint32_t j = 0; j < kResSlots; ++j) {
+          // a number past next[j]: the entry moved on while this block had no
           // frames in its batches (the host waits for the blocks that do)
-          // (relaxed: the poll bypasses the caches without invalidating them;
-          // the acquire is the fence below, once a batch with frames is here)
-          const uint64_t w = __hip_atomic_load(&e.seqn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if ((w >> 16) >= seq) {
-            c = w >> 16;
-            n = static_cast<uint32_t>(w & 0xFFFF);
-            break;
+          if (!got && j < E && (w[j] >> 16) >= next[j]) {
+            got = true;
+            c = w[j] >> 16;
+            n = static_cast<uint32_t>(w[j] & 0xFFFF);
+            b = b0 + j * stride;
+            next[j] = c + kResSlots;
           }
-          const uint64_t now = wall_clock64();
-          if (__hip_atomic_load(&ra.dev->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-              __hip_atomic_load(&ra.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-              now - last > ra.idle_ticks || now - t0 > ra.life_ticks) {
-            __hip_atomic_store(&ra.dev->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
         }
-        if (c != kResQuit) {
-          // (the header is read only by a block with frames: the host cannot
-          // rewrite it before that block's done; a block without frames skips
-          // the fence, whose cache invalidation would cost the XCD's busy blocks)
-          hdr[3] = g < res_used_blocks(n, G);
-          hdr[0] = hdr[3] ? n : 0;
-          if (hdr[3]) {
-            // the host's writes of this batch (header, descriptors, frames), seen from this CU
-            if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
-            hdr[1] = static_cast<uint32_t>(__hip_atomic_load(&e.fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-            hdr[2] = __hip_atomic_load(&e.payload_mult, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
+        if (got) break;
+        // (a signed difference: another block's latest batch may have ended
+        // after this block read the clock)
+        const int64_t idle = static_cast<int64_t>(now - (act > last ? act : last));
+        if ((act == kResQuit) | (stop != 0) | (idle > static_cast<int64_t>(ra.idle_ticks)) |
+            (now - t0 > ra.life_ticks)) {
+          __hip_atomic_fetch_max(&L->act, kResQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (c != kResQuit) {
+        // (the header is read only by a block with frames: the host cannot
+        // rewrite it before that block's done; a block without frames skips
+        // the fence, whose cache invalidation would cost the XCD's busy blocks)
+        hdr[3] = g < res_used_blocks(n, G);
+        hdr[0] = hdr[3] ? n : 0;
+        hdr[4] = b;
+        if (hdr[3]) {
+          // the host's writes of this batch (header, descriptors, frames), seen from this CU
+          if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
+          // fwd and payload_mult in one 8-byte load (one round trip)
+          const uint64_t fm = __hip_atomic_load(reinterpret_cast<uint64_t *>(&R.in[b].fwd), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_SYSTEM);
+          hdr[1] = static_cast<uint32_t>(fm);
+          hdr[2] = static_cast<uint32_t>(fm >> 32);
         }
       }
       cmd = c;
@@ -2179,12 +2224,28 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
     const uint64_t c = cmd;
     if (c == kResQuit) break;
     {
-      KernelArgs a = ra.base;
-      a.descs = ra.descs + static_cast<size_t>(b) * kResFrames;
-      a.verdicts = ra.verdicts + static_cast<size_t>(b) * kResFrames;
-      a.n = min(hdr[0], kResFrames);
-      a.fwd_verdict = static_cast<int32_t>(hdr[1]);
-      a.payload_mult = hdr[2];
+      const uint32_t b = uniform_u32(hdr[4]);
+      // the ring's UMEM is host memory mapped over PCIe: every check in-line as
+      // a 2-byte store (byte enables, no read-modify-write); the store modes are
+      // constants here, so only the ring's pointers take (scalar) registers
+      KernelArgs a;
+      a.umem = uniform_ptr(R.umem);
+      a.umem_size = uniform_u64(R.umem_size);
+      xsknf_gpu_desc *const descs = uniform_ptr(R.descs);
+      a.descs = descs + static_cast<size_t>(b) * kResFrames;
+      a.verdicts = uniform_ptr(R.verdicts) + static_cast<size_t>(b) * kResFrames;
+      a.dummy = reinterpret_cast<const uint4 *>(descs);
+      a.n = min(uniform_u32(hdr[0]), kResFrames);
+      a.fwd_verdict = static_cast<int32_t>(uniform_u32(hdr[1]));
+      a.payload_mult = uniform_u32(hdr[2]);
+      a.defer_min_len = kNoDefer;
+      a.no_scatter = 0;
+      a.seq = 0;
+      a.count_records = 0;
+      a.sector_stores = 0;
+      a.plain_sector = 0;
+      a.tail_scatter = 0;
+      a.store_unchanged = 0;
       // the group's blocks deal the batch in 64-frame rounds: block g takes
       // frames [64 g, 64 g + 64) of a batch of up to 256
       if (a.n) group_tiles<kResLpf, kResNch, kResSpt>(a, g, G);
@@ -2192,13 +2253,17 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
       if (threadIdx.x == 0) {
         if (hdr[3]) {
           if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
-          __hip_atomic_store(&o.done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&uniform_ptr(R.out)[b * kResGroup + g].done, c, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
         }
         last = wall_clock64();
+        __hip_atomic_fetch_max(&L->act, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    seq = c + kResSlots;
   }
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(&L->exits, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ra.blocks - 1)
+    __hip_atomic_store(&ra.ctl->exited, ra.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- host side ----------------------------------------------------------------
@@ -2268,8 +2333,12 @@ uint32_t grid_blocks(K kernel, uint32_t n, int blocks_per_cu, uint32_t tile_fram
   return need < cap ? need : cap;
 }
 
+int resident_blocks_per_cu() { return resident_blocks(reinterpret_cast<const void *>(resident_kernel), kBlock); }
+int device_cu_count() { return device_cus(); }
+
 int launch_resident(const ResArgs &ra, hipStream_t stream) {
-  hipLaunchKernelGGL(resident_kernel, dim3(kResSlots * ra.group), dim3(kBlock), 0, stream, ra);
+  if (ra.blocks == 0 || ra.blocks > kResMaxBlocks) { set_error_text("resident_kernel: bad grid"); return -EINVAL; }
+  hipLaunchKernelGGL(resident_kernel, dim3(ra.blocks), dim3(kBlock), 0, stream, ra);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_error(e, "resident_kernel launch"); return -EIO; }
   return 0;

@@ -52,14 +52,17 @@ void set_error(hipError_t e, const char *where);
 void set_error_text(const char *text);
 
 // ---- the resident worker (XSKNF_GPU_PATH_RESIDENT, host_path.hip) ----------
-// A kernel that stays on the device and takes small batches from a ring in
-// host memory, a group of kResGroup 4-wave blocks per ring entry: the host
-// writes a batch's descriptors and header into entry seq % kResSlots and
-// publishes seq; the entry's blocks poll for it, checksum the batch over PCIe
-// in the mapped UMEM (the register kernel's tiles, dealt over the group:
-// group_tiles) and each publishes its own `done`.  No launch
-// per batch, and up to kResSlots batches in flight at once: the ~10 us launch
-// and completion round trip of a small batch becomes a doorbell and a flag.
+// ONE kernel per device stays resident and serves the rings of every RESIDENT
+// context on that device (one per worker and UMEM: up to kResMaxRings).  Each
+// ring has kResSlots entries; a group of `group` 4-wave blocks serves each
+// entry: the host writes a batch's descriptors and header into entry
+// seq % kResSlots and publishes seq; the entry's blocks poll for it, checksum
+// the batch over PCIe in the mapped UMEM (the register kernel's tiles, dealt
+// over the group: group_tiles) and each publishes its own `done`.  No launch
+// per batch, and up to kResSlots batches per ring in flight at once: the ~10 us
+// launch and completion round trip of a small batch becomes a doorbell and a
+// flag.  When the rings would need more blocks than the kernel may hold
+// (ResArgs::entries_per_block), a block serves several entries of its ring.
 #ifndef XSKNF_RES_SLOTS   // (A/B: tools/ab_resring.sh)
 #define XSKNF_RES_SLOTS 8
 #define XSKNF_RES_FRAMES 256
@@ -69,8 +72,10 @@ void set_error_text(const char *text);
 #endif
 constexpr uint32_t kResSlots = XSKNF_RES_SLOTS;     // ring entries
 constexpr uint32_t kResFrames = XSKNF_RES_FRAMES;   // frames per entry (a larger batch takes several)
-constexpr uint32_t kResGroup = XSKNF_RES_GROUP;     // blocks per entry: the resident kernel has
-constexpr uint32_t kResBlocks = kResSlots * kResGroup;   // kResSlots x kResGroup blocks
+constexpr uint32_t kResGroup = XSKNF_RES_GROUP;     // blocks per entry at most
+constexpr uint32_t kResBlocks = kResSlots * kResGroup;   // done flags per ring (entry x kResGroup + g)
+constexpr uint32_t kResMaxRings = 64;        // XSKNF_MAX_WORKERS (32) x a zero-copy and a copy-mode UMEM
+constexpr uint32_t kResMaxBlocks = 1024;     // grid limit of the resident kernel (and the device's share)
 constexpr uint64_t kResQuit = ~0ull;
 constexpr uint32_t kResBlockFrames = 64;   // frames one block takes per round (4 waves x 16-frame tiles)
 // blocks of an entry (`group` of them) with frames of an n-frame batch: only
@@ -86,39 +91,57 @@ struct alignas(64) ResIn {     // host -> device: the entry's header.  Coherent 
                                // through the BAR, so the polls and header reads stay on the device
   uint64_t seqn;               // the entry's batch (release): ring sequence number (from 1) << 16 | frames,
                                // one word, so a block reads the count that belongs to the number
-  int32_t fwd;                 // forward verdict (prepare()), written before seqn
-  uint32_t payload_mult;
+  int32_t fwd;                 // forward verdict (prepare()), written before seqn; with payload_mult
+  uint32_t payload_mult;       // one 8-byte word the kernel reads with one load
   uint32_t pad[12];
 };
 
-struct alignas(64) ResOut {    // device -> host, one per block: host memory, coherent and mapped
+struct alignas(64) ResOut {    // device -> host, one per (entry, block of its group): host memory
   uint64_t done;               // seq once the block's share of the batch is complete (release)
   uint64_t pad[7];
 };
 
-struct alignas(64) ResCtl {    // host memory, coherent and mapped
+struct alignas(64) ResCtl {    // host memory, coherent and mapped, one per device
   uint64_t stop;               // host -> device: exit now
-  uint64_t pad[7];
+  uint64_t pad0[7];
+  uint64_t exited;             // device -> host: the epoch of the launch whose last block has left
+  uint64_t pad1[7];
 };
 
-struct ResDev {                // device memory, zeroed by the host before each launch
-  uint32_t quit;               // a block has left: every block leaves at its next poll
+struct ResRing {               // one RESIDENT context's ring, as the kernel sees it
+  uint8_t *umem;               // the context's mapped UMEM (checks in-line as 2-byte stores; n / fwd /
+  uint64_t umem_size;          // mult per batch from the entry's header)
+  ResIn *in;                   // headers (kResSlots) and, beside them, descriptors (kResSlots x kResFrames)
+  xsknf_gpu_desc *descs;
+  ResOut *out;                 // done flags (kResBlocks) and verdicts (kResSlots x kResFrames): host memory
+  int32_t *verdicts;
+  uint32_t group;              // blocks per entry: 1, or kResGroup (fixed for the ring's life: the host
+  uint32_t pad;                // waits for res_used_blocks(n, group) flags per batch)
+};
+
+struct ResLaunch {             // device memory, written by the host before each launch
+  uint64_t act;                // device-wide activity: the clock of the last batch any block finished
+                               // (atomic max); kResQuit once a block has left (every block then leaves)
+  uint32_t exits;              // blocks that have left (the last one reports the epoch in ResCtl)
+  uint32_t pad[13];
+  ResRing ring[kResMaxRings];
+  uint32_t block[kResMaxBlocks];                  // blockIdx -> ring << 16 | g << 8 | first entry
+  uint64_t start[kResMaxRings][kResBlocks];       // the first sequence number per (ring, entry x kResGroup + g)
 };
 
 struct ResArgs {
-  KernelArgs base;             // the mapped UMEM and the in-line store modes; n / fwd / mult per batch
-  ResIn *in;                   // device views: headers and descriptors (beside ResIn) ...
-  xsknf_gpu_desc *descs;       // kResSlots x kResFrames
-  ResOut *out;                 // ... completion flags (kResBlocks) and verdicts (host memory)
-  int32_t *verdicts;           // kResSlots x kResFrames
-  ResCtl *ctl;
-  ResDev *dev;
-  uint64_t start[kResBlocks];  // per block (entry x kResGroup + g): the first sequence number it processes
-  uint32_t group;              // blocks per entry in this launch: 1 or kResGroup
-  uint64_t idle_ticks;         // exit after this long without a batch (100 MHz wall clock) ...
+  ResLaunch *L;
+  ResCtl *ctl;                 // device view of the device's ResCtl
+  uint64_t epoch;              // this launch's number (ResCtl::exited)
+  uint32_t blocks;             // grid size
+  uint32_t entries_per_block;  // 1, 2, 4 or 8: a block serves entries b, b + kResSlots / E, ...
+  uint64_t idle_ticks;         // exit after this long without a batch on any ring (100 MHz clock) ...
   uint64_t life_ticks;         // ... or after this long in all; the host relaunches on demand
 };
 
 int launch_resident(const ResArgs &ra, hipStream_t stream);
+// blocks of the resident kernel one CU holds (occupancy), for the grid's cap
+int resident_blocks_per_cu();
+int device_cu_count();
 
 }  // namespace xsknf_gpu

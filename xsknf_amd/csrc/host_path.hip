@@ -42,19 +42,22 @@
 //   share it (their frames are distinct, and a run's gap bytes are the host's
 //   own bytes).
 //
-// RESIDENT: ZEROCOPY, but no batch launches a kernel: a resident kernel
-//   (checksummer.hip resident_kernel) takes the batches from a ring, in entries
-//   of up to kResFrames frames, one 4-wave block per entry, so several batches
-//   (or the pieces of a larger one) are processed at once.  The ring's headers
-//   and descriptors sit in device memory the host writes through the BAR
-//   (large-BAR devices) or in mapped host memory; completion flags and
-//   verdicts in host memory.  submit() writes the descriptors and the entry's
-//   header and publishes its sequence number; wait() spins on the entry's
-//   `done`.  The kernel exits when idle or old (or at destroy) and submit() /
-//   wait() relaunch it from each entry's first batch not done, so a worker
-//   pays a launch only after a pause in its traffic.  No batch takes the
-//   launch path, whose kernels could queue behind the resident one
-//   (resident_acquire).
+// RESIDENT: ZEROCOPY, but no batch launches a kernel: ONE resident kernel per
+//   device (checksummer.hip resident_kernel, host side ResService below) takes
+//   the batches of every RESIDENT context on the device from each context's
+//   ring, in entries of up to kResFrames frames, a group of one or four 4-wave
+//   blocks per entry, so several batches (or the pieces of a larger one) are
+//   processed at once.  Each ring's headers and descriptors sit in device
+//   memory the host writes through the BAR (large-BAR devices) or in mapped
+//   host memory; completion flags and verdicts in host memory.  submit()
+//   writes the descriptors and the entry's header and publishes its sequence
+//   number; wait() spins on the entry's `done`.  The kernel exits when every
+//   ring is idle, when old, or when a ring joins or leaves, and the next
+//   submit() / wait() of any context relaunches it from each entry's first
+//   batch not done, so a worker pays a launch only after a pause in the
+//   device's traffic.  No batch takes the launch path, and the device's
+//   RESIDENT contexts share one stream (one hardware queue), however many
+//   workers there are (up to kResMaxRings rings per device).
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
@@ -64,6 +67,7 @@
 #include <immintrin.h>
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -126,41 +130,23 @@ struct xsknf_gpu_ctx {
   int next = 0;                             // slot the next piece goes to (round robin)
   uint64_t seq = 0;                         // pieces submitted
   xsknf_gpu_ctx_stats stats = {};
-  // RESIDENT: the ring (host memory, coherent, mapped) and the kernel's state
+  // RESIDENT: the context's ring; the kernel and its launches belong to the
+  // device's ResService
   xsknf_gpu::ResIn *rin = nullptr;          // headers + descriptors: host memory, or device memory (BAR)
   xsknf_gpu_desc *rdescs = nullptr;
   bool rbar = false;                        // rin / rdescs are device memory written through the BAR
   xsknf_gpu::ResOut *rout = nullptr;        // completion flags + verdicts: host memory
   int32_t *rverd = nullptr;
-  xsknf_gpu::ResCtl *rctl = nullptr;
-  xsknf_gpu::ResArgs ra = {};               // device views, filled at creation / registration
-  xsknf_gpu::ResDev *rdev = nullptr;
-  xsknf_gpu::ResDev *rinit = nullptr;        // pinned: the state each launch starts from
-  hipStream_t rstream = nullptr;
-  hipEvent_t rdone = nullptr;               // recorded after each launch of the resident kernel
-  bool rlaunched = false;
+  xsknf_gpu::ResRing rring = {};            // the kernel's view, filled at creation / registration
+  int ring_idx = -1;                        // index in the service's ring table (registered)
+  std::atomic<uint64_t> pub[xsknf_gpu::kResSlots] = {};   // last ring number published per entry (relaunch)
   uint64_t rseq = 0;                        // ring entries published
+  int failed = 0;                           // -ETIMEDOUT once a batch never completed: every later
+                                            // call returns it at once
   RingEntry ring[xsknf_gpu::kResSlots];
-  uint64_t relaunches = 0;
 };
 
 namespace {
-
-// A resident kernel holds its hardware queue, and streams beyond the device's
-// hardware queues (GPU_MAX_HW_QUEUES, 4 by default) share them: a launch on a
-// stream sharing the queue would wait behind the resident kernel until it
-// idles out.  So at most kMaxResident RESIDENT contexts per device (one
-// stream each); further ones run as ZEROCOPY.
-constexpr int kMaxResident = 3;
-std::atomic<int> g_resident[64];
-
-bool resident_acquire(int device) {
-  if (device < 0 || device >= 64) return false;
-  int v = g_resident[device].load();
-  while (v < kMaxResident)
-    if (g_resident[device].compare_exchange_weak(v, v + 1)) return true;
-  return false;
-}
 
 int fail(hipError_t e, const char *where) {
   xsknf_gpu::set_error(e, where);
@@ -169,6 +155,200 @@ int fail(hipError_t e, const char *where) {
 
 uint64_t umem_offset(uint64_t addr) {
   return (addr & XSKNF_GPU_UNALIGNED_BUF_ADDR_MASK) + (addr >> XSKNF_GPU_UNALIGNED_BUF_OFFSET_SHIFT);
+}
+
+// ---- RESIDENT: the device's one resident kernel (ResService) --------------------
+//
+// Every RESIDENT context of a device registers its ring here; one kernel on
+// one stream serves them all (checksummer.hip resident_kernel), so the number
+// of workers does not multiply hardware queues or kernels.  The table of rings,
+// the block map and each entry's first sequence number go to the device
+// (ResLaunch) before each launch.  Whoever finds the kernel gone (its last
+// block wrote the launch's epoch to ctl->exited) relaunches it under the
+// service's mutex; adding or removing a ring stops the kernel (ctl->stop),
+// changes the table and relaunches.  A ring's group (blocks per entry) is fixed
+// for its life -- its host side waits for that many done flags per batch --
+// while the entries per block are chosen per launch to fit the grid cap.
+
+// Short lives: a launch on another stream that shares the resident kernel's
+// hardware queue waits behind it, so the kernel leaves every few ms (a relaunch
+// costs one launch, ~0.5 % of a busy ring's time) and after 1 ms without a
+// batch on any ring.
+constexpr uint64_t kResIdleTicks = 100000;      // 1 ms without a batch (100 MHz wall clock)
+constexpr uint64_t kResLifeTicks = 400000;      // 4 ms
+
+struct ResService {
+  std::mutex mu;
+  bool init = false;
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;                 // recorded after each launch
+  xsknf_gpu::ResLaunch *L = nullptr;         // device memory
+  xsknf_gpu::ResLaunch *Lh = nullptr;        // pinned: what the next launch copies to L
+  xsknf_gpu::ResCtl *ctl = nullptr;          // host memory, mapped
+  xsknf_gpu::ResCtl *ctl_dev = nullptr;
+  std::atomic<bool> launched{false};
+  std::atomic<uint64_t> epoch{0};            // the latest launch's number
+  xsknf_gpu_ctx *rings[xsknf_gpu::kResMaxRings] = {};
+  uint32_t cap = 0;                          // blocks the kernel may have
+  std::atomic<uint64_t> launches{0};
+};
+ResService g_svc[64];
+
+// Is the kernel of the latest launch still there (no block has reported its exit)?
+bool svc_running(ResService &s) {
+  return s.launched.load(std::memory_order_acquire) &&
+         __atomic_load_n(&s.ctl->exited, __ATOMIC_ACQUIRE) != s.epoch.load(std::memory_order_acquire);
+}
+
+int svc_init_locked(ResService &s, int device) {
+  using namespace xsknf_gpu;
+  if (s.init) return 0;
+  hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc(&s.L, sizeof(ResLaunch));
+  if (e == hipSuccess) e = hipHostMalloc(&s.Lh, sizeof(ResLaunch), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc(&s.ctl, sizeof(ResCtl), hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.ctl_dev), s.ctl, 0);
+  if (e != hipSuccess) {
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.L) (void)hipFree(s.L);
+    if (s.Lh) (void)hipHostFree(s.Lh);
+    if (s.ctl) (void)hipHostFree(s.ctl);
+    s.done = nullptr, s.stream = nullptr, s.L = nullptr, s.Lh = nullptr, s.ctl = nullptr;
+    return fail(e, "resident service");
+  }
+  memset(s.ctl, 0, sizeof(ResCtl));
+  memset(s.Lh, 0, sizeof(ResLaunch));
+  // at most half the blocks the device holds of this kernel: the resident
+  // kernel must never fill the CUs other work needs
+  const int per_cu = resident_blocks_per_cu();
+  const uint32_t cap = static_cast<uint32_t>(std::max(1, per_cu) * device_cu_count() / 2);
+  s.cap = std::max<uint32_t>(kResSlots, std::min(cap, kResMaxBlocks));
+  s.device = device;
+  s.init = true;
+  return 0;
+}
+
+// Stop the kernel (if there) and wait for it to leave.
+int svc_stop_locked(ResService &s) {
+  if (!s.launched.load()) return 0;
+  __atomic_store_n(&s.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  const hipError_t e = hipEventSynchronize(s.done);
+  s.launched.store(false, std::memory_order_release);
+  if (e != hipSuccess) return fail(e, "resident kernel");
+  return 0;
+}
+
+// The first sequence number block (entry b, g) of ring c takes: the entry's
+// latest batch if published and not done by that block, else the entry's next
+// number (a block that left has finished every batch it took).
+uint64_t ring_start(const xsknf_gpu_ctx *c, uint32_t b, uint32_t g) {
+  using namespace xsknf_gpu;
+  const uint64_t p = c->pub[b].load(std::memory_order_acquire);
+  if (p == 0) return b ? b : kResSlots;   // the entry's first number (they start at 1)
+  if (__atomic_load_n(&c->rout[b * kResGroup + g].done, __ATOMIC_ACQUIRE) == p) return p + kResSlots;
+  return p;
+}
+
+// Launch the kernel over every registered ring (the previous launch, if any,
+// is over: its exit was reported, or it was stopped).
+int svc_launch_locked(ResService &s) {
+  using namespace xsknf_gpu;
+  if (s.launched.load()) {
+    const hipError_t e = hipEventSynchronize(s.done);   // its last block has reported; the grid ends now
+    s.launched.store(false, std::memory_order_release);
+    if (e != hipSuccess) return fail(e, "resident kernel");
+  }
+  uint32_t need = 0, rings = 0;
+  for (const xsknf_gpu_ctx *c : s.rings)
+    if (c) need += kResSlots * c->rring.group, ++rings;
+  if (!rings) return 0;
+  uint32_t E = 1;
+  while (E < kResSlots && need / E > s.cap) E *= 2;
+  const uint32_t stride = kResSlots / E;
+  ResLaunch &h = *s.Lh;
+  h.act = 0;
+  h.exits = 0;
+  uint32_t blk = 0;
+  for (uint32_t r = 0; r < kResMaxRings; ++r) {
+    const xsknf_gpu_ctx *c = s.rings[r];
+    if (!c) continue;
+    h.ring[r] = c->rring;
+    // entry-minor order: blocks are dealt to the XCDs round robin, so a ring's
+    // entries' first blocks (the only ones a batch of <= 64 frames uses) land
+    // on consecutive XCDs
+    for (uint32_t g = 0; g < c->rring.group; ++g)
+      for (uint32_t b = 0; b < stride; ++b) h.block[blk++] = r << 16 | g << 8 | b;
+    for (uint32_t b = 0; b < kResSlots; ++b)
+      for (uint32_t g = 0; g < c->rring.group; ++g) h.start[r][b * kResGroup + g] = ring_start(c, b, g);
+  }
+  hipError_t e = hipMemcpyAsync(s.L, s.Lh, sizeof(ResLaunch), hipMemcpyHostToDevice, s.stream);
+  if (e != hipSuccess) return fail(e, "hipMemcpyAsync(resident table)");
+  __atomic_store_n(&s.ctl->stop, 0ull, __ATOMIC_RELEASE);
+  ResArgs ra = {};
+  ra.L = s.L;
+  ra.ctl = s.ctl_dev;
+  ra.epoch = s.epoch.load() + 1;
+  ra.blocks = blk;
+  ra.entries_per_block = E;
+  ra.idle_ticks = kResIdleTicks;
+  ra.life_ticks = kResLifeTicks;
+  int rc = launch_resident(ra, s.stream);
+  if (rc) return rc;
+  e = hipEventRecord(s.done, s.stream);
+  if (e != hipSuccess) return fail(e, "hipEventRecord(resident)");
+  s.epoch.store(ra.epoch, std::memory_order_release);
+  s.launched.store(true, std::memory_order_release);
+  s.launches += 1;
+  return 0;
+}
+
+// Make sure the kernel is there (cheap when it is: two loads).
+int svc_ensure(xsknf_gpu_ctx *c) {
+  ResService &s = g_svc[c->device];
+  if (svc_running(s)) return 0;
+  std::lock_guard<std::mutex> lk(s.mu);
+  if (svc_running(s)) return 0;
+  return svc_launch_locked(s);
+}
+
+// Register a context's ring (at UMEM registration) and relaunch with it.
+int svc_add(xsknf_gpu_ctx *c) {
+  using namespace xsknf_gpu;
+  if (c->device < 0 || c->device >= 64) return -EINVAL;
+  ResService &s = g_svc[c->device];
+  std::lock_guard<std::mutex> lk(s.mu);
+  int rc = svc_init_locked(s, c->device);
+  if (rc) return rc;
+  int idx = -1;
+  uint32_t min_blocks = c->rring.group;     // at 8 entries per block
+  for (uint32_t r = 0; r < kResMaxRings; ++r) {
+    if (!s.rings[r] && idx < 0) idx = static_cast<int>(r);
+    if (s.rings[r]) min_blocks += s.rings[r]->rring.group;
+  }
+  if (idx < 0 || min_blocks > s.cap) {
+    set_error_text("resident service: no room for another ring on this device");
+    return -ENOSPC;
+  }
+  rc = svc_stop_locked(s);
+  if (rc) return rc;
+  s.rings[idx] = c;
+  c->ring_idx = idx;
+  return svc_launch_locked(s);
+}
+
+// Take a context's ring out (every batch of it complete, or the context
+// failed); the other rings go on in a new launch.
+void svc_remove(xsknf_gpu_ctx *c) {
+  if (c->ring_idx < 0) return;
+  ResService &s = g_svc[c->device];
+  std::lock_guard<std::mutex> lk(s.mu);
+  (void)svc_stop_locked(s);
+  s.rings[c->ring_idx] = nullptr;
+  c->ring_idx = -1;
+  (void)svc_launch_locked(s);
 }
 
 void release(xsknf_gpu_ctx *c) {
@@ -181,19 +361,10 @@ void release(xsknf_gpu_ctx *c) {
     if (s.rec) (void)hipHostFree(s.rec);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
-  if (c->rctl && c->rlaunched) {
-    __atomic_store_n(&c->rctl->stop, 1ull, __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(c->rstream);
-  }
-  if (c->path == XSKNF_GPU_PATH_RESIDENT && c->device >= 0 && c->device < 64) g_resident[c->device].fetch_sub(1);
-  if (c->rdone) (void)hipEventDestroy(c->rdone);
-  if (c->rstream) (void)hipStreamDestroy(c->rstream);
+  svc_remove(c);   // the kernel no longer reads this ring
   if (c->rin) (void)(c->rbar ? hipFree(c->rin) : hipHostFree(c->rin));   // rdescs lies in the same block
   if (c->rout) (void)hipHostFree(c->rout);
   if (c->rverd) (void)hipHostFree(c->rverd);
-  if (c->rctl) (void)hipHostFree(c->rctl);
-  if (c->rdev) (void)hipFree(c->rdev);
-  if (c->rinit) (void)hipHostFree(c->rinit);
   if (c->registered) (void)hipHostUnregister(c->umem_host);
   if (c->path == XSKNF_GPU_PATH_STAGED && c->umem_dev) (void)hipFree(c->umem_dev);
   delete c;
@@ -229,82 +400,48 @@ int complete(xsknf_gpu_ctx *c, Slot &s) {
   return 0;
 }
 
-// ---- RESIDENT: the ring --------------------------------------------------------
+// ---- RESIDENT: the context's ring -------------------------------------------------
 
-// Short lives: a launch on another stream that shares the resident kernel's
-// hardware queue waits behind it, so the kernel leaves every few ms (a relaunch
-// costs one launch, ~0.5 % of a busy ring's time) and after 1 ms without a batch.
-constexpr uint64_t kResIdleTicks = 100000;      // 1 ms without a batch (100 MHz wall clock)
-constexpr uint64_t kResLifeTicks = 400000;      // 4 ms
-
-// Launch the resident kernel unless one is running.  Block b starts at entry
-// b's batch if that is published and not done, else at the entry's next
-// sequence number (a block that left has finished every batch it took).
-int ring_launch(xsknf_gpu_ctx *c) {
-  using namespace xsknf_gpu;
-  if (c->rlaunched) {
-    const hipError_t q = hipEventQuery(c->rdone);
-    if (q == hipErrorNotReady) return 0;
-    if (q != hipSuccess) return fail(q, "resident kernel");
-  }
-  ResArgs ra = c->ra;
-  for (uint32_t k = 0; k < kResBlocks; ++k) {
-    const uint32_t b = k / kResGroup;
-    const RingEntry &e = c->ring[b];
-    if (e.rseq == 0)
-      ra.start[k] = b ? b : kResSlots;   // the entry's first sequence number (they start at 1)
-    else if (__atomic_load_n(&c->rout[k].done, __ATOMIC_ACQUIRE) == e.rseq)
-      ra.start[k] = e.rseq + kResSlots;
-    else
-      ra.start[k] = e.rseq;
-  }
-  // (the previous launch, and with it the previous copy from rinit, is complete)
-  c->rinit->quit = 0;
-  hipError_t e = hipMemcpyAsync(c->rdev, c->rinit, sizeof(ResDev), hipMemcpyHostToDevice, c->rstream);
-  if (e != hipSuccess) return fail(e, "hipMemcpyAsync(resident state)");
-  __atomic_store_n(&c->rctl->stop, 0ull, __ATOMIC_RELEASE);
-  ra.idle_ticks = kResIdleTicks;
-  ra.life_ticks = kResLifeTicks;
-  int rc = launch_resident(ra, c->rstream);
-  if (rc) return rc;
-  e = hipEventRecord(c->rdone, c->rstream);
-  if (e != hipSuccess) return fail(e, "hipEventRecord(resident)");
-  c->rlaunched = true;
-  c->relaunches += 1;
-  return 0;
-}
-
-// Wait for a ring entry's batch (relaunching the kernel if it exited before
+// Wait for a ring entry's batch (relaunching the kernel if it left before
 // reaching it) and hand out its verdicts.
 int ring_complete(xsknf_gpu_ctx *c, RingEntry &r) {
   using namespace xsknf_gpu;
   if (!r.busy) return 0;
+  if (c->failed) return c->failed;
   const xsknf_gpu::ResOut *h = c->rout + (r.rseq % kResSlots) * kResGroup;
-  const uint32_t used = res_used_blocks(r.n, c->ra.group);   // the blocks with frames publish done
+  const uint32_t used = res_used_blocks(r.n, c->rring.group);   // the blocks with frames publish done
   const auto all_done = [h, &r, used] {
     for (uint32_t g = 0; g < used; ++g)
       if (__atomic_load_n(&h[g].done, __ATOMIC_ACQUIRE) != r.rseq) return false;
     return true;
   };
+  ResService &s = g_svc[c->device];
   double t0 = 0;
   for (uint32_t spin = 1; !all_done(); ++spin) {
     __builtin_ia32_pause();
     if ((spin & 1023) == 0) {
-      timespec ts;
-      clock_gettime(CLOCK_MONOTONIC, &ts);
-      const double t = ts.tv_sec + 1e-9 * ts.tv_nsec;
-      if (!t0) t0 = t;
-      if (t - t0 > 10.0) {   // the kernel relaunches itself within ~1 s: something is wrong
-        xsknf_gpu::set_error_text("resident kernel: no completion within 10 s");
-        return -ETIMEDOUT;
-      }
-      const hipError_t q = hipEventQuery(c->rdone);
-      if (q == hipSuccess) {
+      if (!svc_running(s)) {
         if (all_done()) break;
-        const int rc = ring_launch(c);   // it exited before this entry
+        const int rc = svc_ensure(c);   // the kernel left before this entry
         if (rc) return rc;
-      } else if (q != hipErrorNotReady) {
-        return fail(q, "resident kernel");
+      }
+      if ((spin & 65535) == 0) {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        const double t = ts.tv_sec + 1e-9 * ts.tv_nsec;
+        if (!t0) t0 = t;
+        const hipError_t q = s.done ? hipEventQuery(s.done) : hipSuccess;
+        if (q != hipSuccess && q != hipErrorNotReady) return fail(q, "resident kernel");
+        if (t - t0 > 10.0) {
+          // every launch lives at most a few ms and is relaunched on demand:
+          // something is wrong.  Stop the kernel so that it writes nothing more
+          // into frames the caller may recycle after this error, and fail every
+          // later call of this context at once.
+          __atomic_store_n(&s.ctl->stop, 1ull, __ATOMIC_RELEASE);
+          c->failed = -ETIMEDOUT;
+          xsknf_gpu::set_error_text("resident kernel: no completion within 10 s");
+          return -ETIMEDOUT;
+        }
       }
     }
   }
@@ -313,14 +450,16 @@ int ring_complete(xsknf_gpu_ctx *c, RingEntry &r) {
   c->stats.batches += 1;
   c->stats.frames += r.n;
   c->stats.bytes_d2h += sizeof(int32_t) * r.n;
+  c->stats.resident_batches += 1;
   return 0;
 }
 
 int ring_submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint32_t ingress_ifindex,
                 const xsknf_csum_opts *opts, int32_t *verdicts) {
   using namespace xsknf_gpu;
+  if (c->failed) return c->failed;
   KernelArgs a;
-  int rc = prepare(a, c->umem_dev, c->umem_size, c->ra.descs, n, ingress_ifindex, opts, c->ra.verdicts);
+  int rc = prepare(a, c->umem_dev, c->umem_size, c->rring.descs, n, ingress_ifindex, opts, c->rring.verdicts);
   if (rc != 0) return rc < 0 ? rc : 0;
   const uint64_t r = c->rseq + 1;
   const uint32_t k = static_cast<uint32_t>(r % kResSlots);
@@ -336,6 +475,7 @@ int ring_submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint3
   if (c->rbar) _mm_sfence();
   __atomic_store_n(&h.seqn, r << 16 | n, __ATOMIC_RELEASE);
   if (c->rbar) _mm_sfence();
+  c->pub[k].store(r, std::memory_order_release);
   c->rseq = r;
   c->stats.bytes_h2d += sizeof(xsknf_gpu_desc) * n;
   e.busy = true;
@@ -343,7 +483,7 @@ int ring_submit(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint3
   e.rseq = r;
   e.n = n;
   e.out = verdicts;
-  return ring_launch(c);
+  return svc_ensure(c);
 }
 
 // Complete every piece / ring batch with a sequence number <= upto, oldest first.
@@ -549,8 +689,11 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
   c->max_batch = max_batch;
   c->slot_frames = std::min(max_batch, kPiece);
   c->hint = frame_len_hint;
+  if (device < 0 || device >= 64) {
+    delete c;
+    return -EINVAL;
+  }
   hipError_t e = hipSetDevice(device);
-  if (path == XSKNF_GPU_PATH_RESIDENT && !resident_acquire(device)) c->path = path = XSKNF_GPU_PATH_ZEROCOPY;
   for (Slot &s : c->slot) {
     if (path == XSKNF_GPU_PATH_RESIDENT) break;   // the ring takes every batch
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
@@ -581,32 +724,24 @@ int xsknf_gpu_ctx_create(struct xsknf_gpu_ctx **out, int device, int path, uint3
     if (e == hipSuccess) c->rdescs = reinterpret_cast<xsknf_gpu_desc *>(c->rin + kResSlots);
     if (e == hipSuccess) e = hipHostMalloc(&c->rout, sizeof(ResOut) * kResBlocks, fl);
     if (e == hipSuccess) e = hipHostMalloc(&c->rverd, sizeof(int32_t) * kResSlots * kResFrames, fl);
-    if (e == hipSuccess) e = hipHostMalloc(&c->rctl, sizeof(ResCtl), fl);
-    if (e == hipSuccess) e = hipMalloc(&c->rdev, sizeof(ResDev));
-    if (e == hipSuccess) e = hipHostMalloc(&c->rinit, sizeof(ResDev), hipHostMallocDefault);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->rdone, hipEventDisableTiming);
     if (e == hipSuccess) {
       for (uint32_t k = 0; k < kResSlots; ++k)   // (host stores: the BAR mapping is the same address)
         c->rin[k].seqn = 0;
       for (uint32_t k = 0; k < kResBlocks; ++k) c->rout[k].done = 0;
       if (c->rbar) _mm_sfence();
-      memset(c->rctl, 0, sizeof(ResCtl));
       if (c->rbar) {
-        c->ra.in = c->rin;
-        c->ra.descs = c->rdescs;
+        c->rring.in = c->rin;
+        c->rring.descs = c->rdescs;
       } else {
-        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.in), c->rin, 0);
-        if (e == hipSuccess) c->ra.descs = reinterpret_cast<xsknf_gpu_desc *>(c->ra.in + kResSlots);
+        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->rring.in), c->rin, 0);
+        if (e == hipSuccess) c->rring.descs = reinterpret_cast<xsknf_gpu_desc *>(c->rring.in + kResSlots);
       }
     }
-    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.out), c->rout, 0);
-    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.verdicts), c->rverd, 0);
-    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->ra.ctl), c->rctl, 0);
-    c->ra.dev = c->rdev;
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->rring.out), c->rout, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->rring.verdicts), c->rverd, 0);
     // batches of up to 64 frames: one block per entry (a group's idle blocks
     // would cost them ~1 us); larger ones: the group deals 64-frame rounds
-    c->ra.group = max_batch <= kResBlockFrames ? 1 : kResGroup;
+    c->rring.group = max_batch <= kResBlockFrames ? 1 : kResGroup;
   }
   if (e != hipSuccess) {
     const int rc = fail(e, "xsknf_gpu_ctx_create");
@@ -641,14 +776,18 @@ int xsknf_gpu_ctx_register_umem(struct xsknf_gpu_ctx *c, void *umem, uint64_t si
     return fail(e, "xsknf_gpu_ctx_register_umem");
   }
   if (c->path == XSKNF_GPU_PATH_RESIDENT) {
-    // the resident kernel's fixed arguments: the mapped UMEM, checks in-line as
-    // 2-byte stores (host memory has byte enables), per-batch fields from the ring
-    using namespace xsknf_gpu;
-    const xsknf_csum_opts o = {1, XSKNF_CSUM_ACTION_DROP, 1, 0};
-    KernelArgs &a = c->ra.base;
-    (void)prepare(a, c->umem_dev, c->umem_size, c->ra.descs, 1, 0, &o, c->ra.verdicts);
-    a.defer_min_len = kNoDefer;
-    a.sector_stores = 0;
+    // the resident kernel's view of the ring: the mapped UMEM (checks in-line as
+    // 2-byte stores: host memory has byte enables), per-batch fields from the ring
+    c->rring.umem = c->umem_dev;
+    c->rring.umem_size = c->umem_size;
+    // the device's resident kernel serves this ring from now on
+    const int rc = svc_add(c);
+    if (rc) {
+      (void)hipHostUnregister(umem);
+      c->registered = false;
+      c->umem_dev = c->umem_mapped = nullptr;
+      return rc;
+    }
   }
   return 0;
 }
@@ -682,6 +821,7 @@ int xsknf_gpu_ctx_process_batch(struct xsknf_gpu_ctx *c, const struct xsknf_gpu_
 int xsknf_gpu_ctx_get_stats(const struct xsknf_gpu_ctx *c, struct xsknf_gpu_ctx_stats *stats) {
   if (!c || !stats) return -EINVAL;
   *stats = c->stats;
+  if (c->path == XSKNF_GPU_PATH_RESIDENT) stats->resident_launches = g_svc[c->device].launches.load();
   return 0;
 }
 
@@ -834,6 +974,8 @@ int xsknf_gpu_hook_get_stats(const struct xsknf_gpu_hook *h, uint32_t worker_idx
     stats->frames += s.ctx->stats.frames;
     stats->bytes_h2d += s.ctx->stats.bytes_h2d;
     stats->bytes_d2h += s.ctx->stats.bytes_d2h;
+    stats->resident_batches += s.ctx->stats.resident_batches;
+    if (s.ctx->path == XSKNF_GPU_PATH_RESIDENT) stats->resident_launches = g_svc[s.ctx->device].launches.load();
   }
   return 0;
 }
