@@ -2116,9 +2116,10 @@ __global__ __launch_bounds__(kBlock) void scatter_checks(const KernelArgs args) 
 // batches ~1 us.  A block without frames reads nothing but the word and moves
 // on; it may find the entry already past it (the host waits only for the
 // blocks with frames), and then takes the newer number.
-// A block leaves when the host sets ctl->stop (a ring joins or leaves), when
+// A block leaves when the host sets the stop word (a ring joins or leaves), when
 // NO block has finished a batch for idle_ticks (ResLaunch::act, the clock of
-// the latest batch, kept by an atomic max), or after life_ticks in all; it
+// the latest batch, kept by an atomic max at most every idle_ticks / 8 per
+// block), or after life_ticks in all; it
 // tells the others by setting act to kResQuit, and the last block to leave
 // reports the launch's epoch in ctl->exited.  A batch published to a kernel
 // that has left waits for the host to relaunch it (every block then starts at
@@ -2132,9 +2133,16 @@ __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return __builtin_a
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
   return static_cast<uint64_t>(uniform_u32(static_cast<uint32_t>(v >> 32))) << 32 | uniform_u32(static_cast<uint32_t>(v));
 }
+// ... and known to address global memory: a pointer read from LDS is generic,
+// and every access through it would be a FLAT instruction (both counters, no
+// scalar base); made from the integer as a global pointer, then cast to
+// generic, its uses get the GLOBAL forms from the compiler's address-space
+// inference, as kernel arguments do.
 template <typename T>
 __device__ __forceinline__ T *uniform_ptr(T *p) {
-  return reinterpret_cast<T *>(uniform_u64(reinterpret_cast<uint64_t>(p)));
+  typedef __attribute__((address_space(1))) T gT;
+  gT *const q = (gT *)uniform_u64(reinterpret_cast<uint64_t>(p));   // an integer made a global pointer ...
+  return (T *)q;                                                     // ... then generic: inferable
 }
 #ifndef XSKNF_RES_FENCE   // A/B timing only: 0 drops the system-scope cache maintenance (unsafe)
 #define XSKNF_RES_FENCE 1
@@ -2144,16 +2152,22 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
   static_assert(kResBlockFrames == kWavesPerBlock * kResSpt * (kWave / kResLpf), "one round per block");
   __shared__ uint64_t cmd;
   __shared__ uint32_t hdr[5];
-  // the block's ring, copied to LDS once: the system-scope acquire of every
-  // batch invalidates the caches, and the ring's pointers would be re-read
-  // from memory behind it on each batch's critical path
-  __shared__ ResRing R;
+  // the block's ring, read once into scalar registers: the system-scope
+  // acquire of every batch invalidates the caches, and the ring's pointers
+  // would be re-read from memory behind it on each batch's critical path
+  // (read through ra.rings, a read-only view: the compiler then knows them to
+  // be global pointers and uses the GLOBAL forms, not FLAT)
   ResLaunch *const L = ra.L;
   const uint32_t m = L->block[blockIdx.x];
   const uint32_t r = m >> 16, g = (m >> 8) & 0xff, b0 = m & 0xff;
-  if (threadIdx.x == 0) R = L->ring[r];
-  __syncthreads();
-  const uint32_t G = R.group;
+  const ResRing &Rg = ra.rings[r];
+  uint8_t *const r_umem = uniform_ptr(Rg.umem);
+  const uint64_t r_umem_size = uniform_u64(Rg.umem_size);
+  ResIn *const in = uniform_ptr(Rg.in);
+  xsknf_gpu_desc *const r_descs = uniform_ptr(Rg.descs);
+  ResOut *const r_out = uniform_ptr(Rg.out);
+  int32_t *const r_verdicts = uniform_ptr(Rg.verdicts);
+  const uint32_t G = uniform_u32(Rg.group);
   const uint32_t E = ra.entries_per_block, stride = kResSlots / E;
   // lane 0's state: the next sequence number of each entry it serves (in LDS:
   // registers live across group_tiles would cost the kernel its second wave per SIMD)
@@ -2162,7 +2176,7 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
     next[threadIdx.x] = threadIdx.x < E ? L->start[r][(b0 + threadIdx.x * stride) * kResGroup + g] : kResQuit;
   __syncthreads();
   const uint64_t t0 = wall_clock64();
-  uint64_t last = t0;
+  uint64_t last = t0, told = t0;   // this block's latest batch; when it last told L->act
   for (;;) {
     if (threadIdx.x == 0) {
       uint64_t c = kResQuit;
@@ -2173,10 +2187,10 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
         uint64_t w[kResSlots];
 #pragma unroll
         for (uint32_t j = 0; j < kResSlots; ++j)
-          w[j] = j < E ? __hip_atomic_load(&R.in[b0 + j * stride].seqn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+          w[j] = j < E ? __hip_atomic_load(&in[b0 + j * stride].seqn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                        : 0;
         const uint64_t act = __hip_atomic_load(&L->act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t stop = __hip_atomic_load(&ra.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t stop = __hip_atomic_load(ra.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint64_t now = wall_clock64();
 #pragma unroll
         for (uint32_t j = 0; j < kResSlots; ++j) {
@@ -2212,7 +2226,7 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
           // the host's writes of this batch (header, descriptors, frames), seen from this CU
           if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
           // fwd and payload_mult in one 8-byte load (one round trip)
-          const uint64_t fm = __hip_atomic_load(reinterpret_cast<uint64_t *>(&R.in[b].fwd), __ATOMIC_RELAXED,
+          const uint64_t fm = __hip_atomic_load(reinterpret_cast<uint64_t *>(&in[b].fwd), __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_SYSTEM);
           hdr[1] = static_cast<uint32_t>(fm);
           hdr[2] = static_cast<uint32_t>(fm >> 32);
@@ -2229,12 +2243,11 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
       // a 2-byte store (byte enables, no read-modify-write); the store modes are
       // constants here, so only the ring's pointers take (scalar) registers
       KernelArgs a;
-      a.umem = uniform_ptr(R.umem);
-      a.umem_size = uniform_u64(R.umem_size);
-      xsknf_gpu_desc *const descs = uniform_ptr(R.descs);
-      a.descs = descs + static_cast<size_t>(b) * kResFrames;
-      a.verdicts = uniform_ptr(R.verdicts) + static_cast<size_t>(b) * kResFrames;
-      a.dummy = reinterpret_cast<const uint4 *>(descs);
+      a.umem = r_umem;
+      a.umem_size = r_umem_size;
+      a.descs = r_descs + static_cast<size_t>(b) * kResFrames;
+      a.verdicts = r_verdicts + static_cast<size_t>(b) * kResFrames;
+      a.dummy = reinterpret_cast<const uint4 *>(r_descs);
       a.n = min(uniform_u32(hdr[0]), kResFrames);
       a.fwd_verdict = static_cast<int32_t>(uniform_u32(hdr[1]));
       a.payload_mult = uniform_u32(hdr[2]);
@@ -2253,11 +2266,16 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
       if (threadIdx.x == 0) {
         if (hdr[3]) {
           if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
-          __hip_atomic_store(&uniform_ptr(R.out)[b * kResGroup + g].done, c, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&r_out[b * kResGroup + g].done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         last = wall_clock64();
-        __hip_atomic_fetch_max(&L->act, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the device-wide activity only needs the idle exit's precision: an
+        // atomic per batch (on one word, from every block) would sit in front
+        // of the next poll's wait
+        if (last - told > ra.idle_ticks / 8) {
+          __hip_atomic_fetch_max(&L->act, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          told = last;
+        }
       }
     }
   }

@@ -102,11 +102,16 @@ struct alignas(64) ResOut {    // device -> host, one per (entry, block of its g
 };
 
 struct alignas(64) ResCtl {    // host memory, coherent and mapped, one per device
-  uint64_t stop;               // host -> device: exit now
+  uint64_t stop;               // host -> device: exit now (unless ResStop is in device memory)
   uint64_t pad0[7];
   uint64_t exited;             // device -> host: the epoch of the launch whose last block has left
   uint64_t pad1[7];
 };
+
+struct alignas(64) ResStop {   // host -> device: exit now.  Fine-grained device memory the host
+  uint64_t stop;               // writes through the BAR (large-BAR devices), so that the blocks'
+  uint64_t pad[7];             // polls of it stay on the device and take nothing from the PCIe
+};                             // reads of the batches; else ResCtl::stop in host memory
 
 struct ResRing {               // one RESIDENT context's ring, as the kernel sees it
   uint8_t *umem;               // the context's mapped UMEM (checks in-line as 2-byte stores; n / fwd /
@@ -131,7 +136,9 @@ struct ResLaunch {             // device memory, written by the host before each
 
 struct ResArgs {
   ResLaunch *L;
+  const ResRing *rings;        // = L->ring, read only: its pointers are then known to be global
   ResCtl *ctl;                 // device view of the device's ResCtl
+  uint64_t *stop;              // device view of the stop word (ResStop, or ResCtl::stop)
   uint64_t epoch;              // this launch's number (ResCtl::exited)
   uint32_t blocks;             // grid size
   uint32_t entries_per_block;  // 1, 2, 4 or 8: a block serves entries b, b + kResSlots / E, ...

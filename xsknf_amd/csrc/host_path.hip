@@ -165,7 +165,7 @@ uint64_t umem_offset(uint64_t addr) {
 // the block map and each entry's first sequence number go to the device
 // (ResLaunch) before each launch.  Whoever finds the kernel gone (its last
 // block wrote the launch's epoch to ctl->exited) relaunches it under the
-// service's mutex; adding or removing a ring stops the kernel (ctl->stop),
+// service's mutex; adding or removing a ring stops the kernel (the stop word),
 // changes the table and relaunches.  A ring's group (blocks per entry) is fixed
 // for its life -- its host side waits for that many done flags per batch --
 // while the entries per block are chosen per launch to fit the grid cap.
@@ -187,6 +187,9 @@ struct ResService {
   xsknf_gpu::ResLaunch *Lh = nullptr;        // pinned: what the next launch copies to L
   xsknf_gpu::ResCtl *ctl = nullptr;          // host memory, mapped
   xsknf_gpu::ResCtl *ctl_dev = nullptr;
+  uint64_t *stop = nullptr;                  // the stop word: ResStop in device memory (BAR), or ctl->stop
+  uint64_t *stop_dev = nullptr;
+  bool stop_bar = false;
   std::atomic<bool> launched{false};
   std::atomic<uint64_t> epoch{0};            // the latest launch's number
   xsknf_gpu_ctx *rings[xsknf_gpu::kResMaxRings] = {};
@@ -221,6 +224,20 @@ int svc_init_locked(ResService &s, int device) {
   }
   memset(s.ctl, 0, sizeof(ResCtl));
   memset(s.Lh, 0, sizeof(ResLaunch));
+  // the stop word where the blocks' polls stay on the device (large BAR), as the rings' headers
+  s.stop = &s.ctl->stop;
+  s.stop_dev = &s.ctl_dev->stop;
+  int large_bar = 0;
+  void *p = nullptr;
+  if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) == hipSuccess && large_bar &&
+      hipExtMallocWithFlags(&p, sizeof(ResStop), hipDeviceMallocFinegrained) == hipSuccess) {
+    s.stop = s.stop_dev = static_cast<uint64_t *>(p);
+    s.stop_bar = true;
+    *s.stop = 0;
+    _mm_sfence();
+  } else {
+    (void)hipGetLastError();
+  }
   // at most half the blocks the device holds of this kernel: the resident
   // kernel must never fill the CUs other work needs
   const int per_cu = resident_blocks_per_cu();
@@ -231,10 +248,15 @@ int svc_init_locked(ResService &s, int device) {
   return 0;
 }
 
+void svc_set_stop(ResService &s, uint64_t v) {
+  __atomic_store_n(s.stop, v, __ATOMIC_RELEASE);
+  if (s.stop_bar) _mm_sfence();   // out of the write-combining buffer
+}
+
 // Stop the kernel (if there) and wait for it to leave.
 int svc_stop_locked(ResService &s) {
   if (!s.launched.load()) return 0;
-  __atomic_store_n(&s.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  svc_set_stop(s, 1);
   const hipError_t e = hipEventSynchronize(s.done);
   s.launched.store(false, std::memory_order_release);
   if (e != hipSuccess) return fail(e, "resident kernel");
@@ -286,10 +308,12 @@ int svc_launch_locked(ResService &s) {
   }
   hipError_t e = hipMemcpyAsync(s.L, s.Lh, sizeof(ResLaunch), hipMemcpyHostToDevice, s.stream);
   if (e != hipSuccess) return fail(e, "hipMemcpyAsync(resident table)");
-  __atomic_store_n(&s.ctl->stop, 0ull, __ATOMIC_RELEASE);
+  svc_set_stop(s, 0);
   ResArgs ra = {};
   ra.L = s.L;
+  ra.rings = s.L->ring;
   ra.ctl = s.ctl_dev;
+  ra.stop = s.stop_dev;
   ra.epoch = s.epoch.load() + 1;
   ra.blocks = blk;
   ra.entries_per_block = E;
@@ -437,7 +461,7 @@ int ring_complete(xsknf_gpu_ctx *c, RingEntry &r) {
           // something is wrong.  Stop the kernel so that it writes nothing more
           // into frames the caller may recycle after this error, and fail every
           // later call of this context at once.
-          __atomic_store_n(&s.ctl->stop, 1ull, __ATOMIC_RELEASE);
+          svc_set_stop(s, 1);
           c->failed = -ETIMEDOUT;
           xsknf_gpu::set_error_text("resident kernel: no completion within 10 s");
           return -ETIMEDOUT;
