@@ -2427,8 +2427,9 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
     // as others end): the static schedule deals each wave every waves-th tile,
     // at most PT of them; a pool block's units (its tiles, the last SW of them
     // halved) are at most SW x PT, and a wave with a full list claims no more.
-    // Waves past their lists wrote in-line in the launches of the three
-    // unexplained illegal-address faults of the GPU suites.
+    // (Kept from the investigation of the GPU suites' illegal-address faults,
+    // whose cause was HIP's locked-pageable-memory copy in the test process,
+    // not these kernels -- DESIGN 3; tested by test_no_wave_passes_its_patch_list.)
     if (a.tail_scatter) {
       const uint32_t tiles = (a.n + kWave - 1) / kWave;
       constexpr uint32_t per_block = SW > kWavesPerBlock ? SW * (PT - 1) : SW * PT;
