@@ -18,9 +18,17 @@
 // traffic carries them: the GPU kernels then write nothing back for all but
 // the carry-loss frames.  Default: random check bytes (every check changes).
 //
+// The feeding thread (this one) is pinned to the last CPU of the process's
+// affinity set once the worker runs (the worker takes the first, as
+// src/xsknf.c:1049-1095 pins workers), so the two never share a core;
+// HOOK_BENCH_FEEDER_CPU=-1 leaves it unpinned.
+//
 // Prints one JSON line.  Tool, not product: it links the oracle only as the CPU
 // NF of mode "cpu" (the reference path, as tools/config1.py does).
+#define _GNU_SOURCE
 #include <arpa/inet.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -163,6 +171,22 @@ int main(int argc, char **argv)
 		fprintf(stderr, "start: %d\n", rc);
 		return 1;
 	}
+	int feeder_cpu = -1;
+	{
+		const char *fc = getenv("HOOK_BENCH_FEEDER_CPU");
+		cpu_set_t set;
+		if ((!fc || atoi(fc) >= 0) && sched_getaffinity(0, sizeof(set), &set) == 0) {
+			for (int c = CPU_SETSIZE - 1; c >= 0; c--)
+				if (CPU_ISSET(c, &set)) {
+					feeder_cpu = fc ? atoi(fc) : c;
+					break;
+				}
+			CPU_ZERO(&set);
+			CPU_SET(feeder_cpu, &set);
+			if (pthread_setaffinity_np(pthread_self(), sizeof(set), &set))
+				feeder_cpu = -1;
+		}
+	}
 	const double t0 = now_s();
 	double tm = 0;
 	uint64_t rx0 = 0;
@@ -189,11 +213,11 @@ int main(int argc, char **argv)
 	xsknf_cleanup();
 	const double mpps = rx / (t1 - tm) / 1e6;
 	printf("{\"checks\": \"%s\", \"mode\": \"%s\", \"len\": %u, \"batch\": %u, \"path\": \"%s\", \"depth\": %u, "
-	       "\"seconds\": %.2f, \"mpps\": %.3f, \"gbps\": %.2f, \"worker_error\": %d}\n",
+	       "\"seconds\": %.2f, \"mpps\": %.3f, \"gbps\": %.2f, \"feeder_cpu\": %d, \"worker_error\": %d}\n",
 	       nic ? "nic" : "random", mode, len, batch,
 	       path == XSKNF_GPU_PATH_STAGED ? "STAGED" : path == XSKNF_GPU_PATH_RESIDENT ? "RESIDENT" : "ZEROCOPY",
 	       depth, t1 - tm, mpps,
-	       mpps * len / 1e3, err);
+	       mpps * len / 1e3, feeder_cpu, err);
 	free(frames);
 	free(txbuf);
 	return err ? 1 : 0;

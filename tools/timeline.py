@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--variant", default="", help="lanes,chunks,u,ring,fused,kernel,window (default: product)")
     ap.add_argument("--bpc", type=int, default=0, help="blocks per CU asked for (0: the shape's own)")
+    ap.add_argument("--same-checks", action="store_true",
+                    help="every launch with -i 1 (after the first visit of a batch its checks are right and "
+                         "nothing is written); default: alternate -i 1 / 2 per visit, so every check changes")
     a = ap.parse_args()
     length, layout = WL.get(a.workload, (int(a.workload) if a.workload.isdigit() else a.workload, "aligned"))
     dev = torch.device("cuda:0")
@@ -53,7 +56,7 @@ def main():
     if not hasattr(lib, "xsknf_gpu_ab_set_timeline"):
         raise SystemExit("not a timeline build: set XSKNF_GPU_LIB=build/tl/libxsknf_gpu.so")
     lib.xsknf_gpu_ab_set_timeline.argtypes = [ctypes.c_void_p]
-    opts = _lib.CsumOpts(1, 0, 1, 0)
+    opts_by_iters = {1: _lib.CsumOpts(1, 0, 1, 0), 2: _lib.CsumOpts(2, 0, 1, 0)}
     cfg = _lib.LaunchCfg()
     lens = lens_all[:n]
     lib.xsknf_gpu_launch_cfg_for_lens(int(lens.max()), int(lens.mean()), ctypes.byref(cfg))
@@ -66,10 +69,15 @@ def main():
     tl = torch.zeros(8 * 65536, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
 
+    visits = [0] * K
+
     def run(j):
+        # (the bench's worst case: each visit of a batch alternates -i 1 / 2, so every check changes)
+        it = 1 if a.same_checks else 1 + visits[j] % 2
+        visits[j] += 1
         rc = lib.xsknf_gpu_checksum_batch_cfg(ctypes.c_void_p(umem.data_ptr()), umem.numel(),
                                               ctypes.c_void_p(descs_all.data_ptr() + 16 * n * j), n, 0,
-                                              ctypes.byref(opts), ctypes.c_void_p(verd.data_ptr()),
+                                              ctypes.byref(opts_by_iters[it]), ctypes.c_void_p(verd.data_ptr()),
                                               ctypes.byref(cfg), ctypes.c_void_p(stream.cuda_stream))
         _lib.check(rc, "launch")
 

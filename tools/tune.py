@@ -36,7 +36,7 @@ from xsknf_amd import _lib, frames  # noqa: E402
 
 WL = {
     "1500": (1500, "aligned"), "64": (64, "aligned"), "imix": ("imix", "aligned"),
-    "jumbo": (9000, "unaligned"), "570": (570, "aligned"),
+    "jumbo": (9000, "unaligned"), "570": (570, "aligned"), "64u": (64, "unaligned"), "60u": (60, "unaligned"),
 }
 
 

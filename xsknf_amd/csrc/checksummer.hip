@@ -679,10 +679,24 @@ constexpr int kLaneSlot = 16 * kHdrChunks;   // per-lane LDS header window
 // Default-policy loads: a lane's chunks of one frame arrive in NCH separate
 // (uncoalesced) instructions, and the line must stay in L2 between them (and
 // for the sector store that follows); non-temporal loads refetch it.
+// Chunks 4 and up are loaded only when some frame of the wave's step reaches
+// them (a wave-uniform branch): a step of 16-byte-aligned 64 B frames then
+// issues 4 load instructions of a 5-chunk window, not 5 (the fifth re-read
+// the fourth chunk: one more instruction's worth of requests per frame), and a
+// step with frames at odd starts still loads its 5 chunks at once.
+// XSKNF_LANE_CLAMP=1 (A/B): every chunk loaded, as before.
+#ifndef XSKNF_LANE_CLAMP
+#define XSKNF_LANE_CLAMP 0
+#endif
 template <int NCH>
 __device__ __forceinline__ void load_lane(const FrameRef &r, uint4 (&v)[NCH]) {
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) v[k] = *XSKNF_GLD(r.cp + min(k, r.nch - 1), 16);
+  for (int k = 0; k < NCH; ++k) {
+    if (XSKNF_LANE_CLAMP || k < 4 || __builtin_amdgcn_ballot_w64(k < r.nch))
+      v[k] = *XSKNF_GLD(r.cp + min(k, r.nch - 1), 16);
+    else
+      v[k] = make_uint4(0, 0, 0, 0);   // past every frame of the step: outside every sum and parse
+  }
 }
 
 // A lane's result; when `sector` is set, the frame's patched 64-byte check
