@@ -143,10 +143,17 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+_DIST = False   # a process group is up (world > 1, or XSKNF_BENCH_DIST=1 at world 1)
+
+
 def dist_setup(args):
     """One process per GPU (torch.distributed.run env).  XSKNF_BENCH_BACKEND=gloo
     rehearses the N > 1 path on fewer GPUs (ranks share devices round robin);
-    the default is nccl (RCCL), one rank per GPU."""
+    the default is nccl (RCCL), one rank per GPU.  XSKNF_BENCH_DIST=1 brings the
+    process group up at world 1 too, so that the collectives (RCCL's init,
+    barrier, device-tensor all-reduces and broadcast, the root-distribution leg)
+    run on a one-GPU box exactly as at N > 1."""
+    global _DIST
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -154,7 +161,8 @@ def dist_setup(args):
     ndev = max(1, torch.cuda.device_count())
     if backend != "nccl":
         local %= ndev
-    if world > 1:
+    _DIST = world > 1 or (os.environ.get("XSKNF_BENCH_DIST") == "1" and "MASTER_ADDR" in os.environ)
+    if _DIST:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -169,7 +177,7 @@ def dist_setup(args):
 
 
 def barrier(world):
-    if world > 1:
+    if _DIST:
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -180,7 +188,7 @@ def coll_device():
 
 
 def allreduce_max(x: float, world: int) -> float:
-    if world == 1:
+    if not _DIST:
         return x
     t = torch.tensor([x], dtype=torch.float64, device=coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -189,7 +197,7 @@ def allreduce_max(x: float, world: int) -> float:
 
 def allreduce_sum_i64(vals, world):
     t = torch.tensor(vals, dtype=torch.int64, device=coll_device())
-    if world > 1:
+    if _DIST:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [int(x) for x in t.tolist()]
 
@@ -712,11 +720,11 @@ def main():
         del r
         torch.cuda.empty_cache()
 
-    root_scatter = root_scatter_leg(args, world, rank, dev) if (world > 1 and not args.no_root_scatter) else None
+    root_scatter = root_scatter_leg(args, world, rank, dev) if (_DIST and not args.no_root_scatter) else None
     # what the collectives saw: every rank contributes 1 (so a SCALE line shows
     # that the backend really had N ranks), and the frames summed over ranks
     dist_info = None
-    if world > 1:
+    if _DIST:
         seen = allreduce_sum_i64([1], world)[0]
         dist_info = {"ranks_seen": seen, "backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
                      "frames_allreduced": prim["counters"][0],
@@ -782,7 +790,7 @@ def main():
         if dist_info is not None:
             out["dist"] = dist_info
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if _DIST:
         dist.destroy_process_group()
 
 

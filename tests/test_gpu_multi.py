@@ -165,3 +165,32 @@ def test_bench_gpus_n_starts_its_ranks(dev, clean_ctx):
     assert line["dist"]["frames_allreduced"] == 2 * 65536
     assert line["root_scatter"]["frames_total"] == 2 * 65536
     assert line["root_scatter"]["vs_single_gpu"]["match"] is True
+
+
+def test_rccl_collectives_on_one_gpu(dev, clean_ctx):
+    """The RCCL branch of bench.py on the MI355X itself: one rank under
+    torch.distributed.run with XSKNF_BENCH_DIST=1 brings the "nccl" process
+    group up (init_process_group(device_id=...)), and the run goes through the
+    same collectives as at N > 1 -- barriers, device-tensor all-reduces, the
+    root distribution's broadcast (`shard.scatter_from_root`, device tensors)
+    and the HIP kernel on the shard it hands back, checked against the
+    single-GPU pass by the fingerprint.  (N > 1 over xGMI needs a multi-GPU
+    node: the driver's SCALE run.)"""
+    port = _free_port()
+    env = dict(os.environ, XSKNF_BENCH_DIST="1")
+    env.pop("XSKNF_BENCH_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", "1", "--steps", "3",
+           "--warmup", "1", "--frames", "65536", "--secondary", "", "--cpu-seconds", "0", "--kernel-steps", "0",
+           "--min-warmup-s", "0", "--no-probes"]
+    with clean_ctx.Pool(1) as pool:
+        rc, out, err = pool.apply(_run, (cmd, env, 400))
+    assert rc == 0, err[-3000:]
+    line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+    assert line["dist"]["backend"] == "nccl"
+    assert line["dist"]["collective_device"] == "cuda"
+    assert line["dist"]["ranks_seen"] == 1 and line["dist"]["world_size"] == 1
+    assert line["dist"]["frames_allreduced"] == 65536
+    assert line["root_scatter"]["frames_total"] == 65536
+    assert line["root_scatter"]["vs_single_gpu"]["match"] is True
+    assert line["root_scatter"]["rfc_check"]["violations"] == 0

@@ -345,8 +345,12 @@ int main(int argc, char **argv)
 	};
 	struct xsknf_gpu_hook *hook = NULL;
 	// small rx batches (the reference's default is 64, src/xsknf.c:49): the
-	// resident kernel's ring, four batches out (NF level, 64-frame batches:
-	// 30.2 vs 12.5 Mpps launched at 64 B, 15.7 vs 11.3 at 1500 B -- DESIGN 5.3)
+	// resident kernel's ring, four batches out.  Set from the NF-level sweep
+	// with the feeder pinned apart (tools/hook_default.sh, medians of 5,
+	// profiles/r04/nf/): at 64 and 128 frames RESIDENT 21.0 / 21.4 Mpps against
+	// 7.9 / 17.5 launched (64 B) and 10.3 / 10.3 against 6.6 / 10.2 (1500 B);
+	// from 256 frames the launched hook is level or ahead (64 B 23.5 vs 21.1,
+	// 1500 B 11.5 vs 11.0 at 256; 22.5 vs 20.8 and 11.6 vs 10.8 at 1024) -- DESIGN 5.3
 	const int small = config.batch_size <= 128;
 	if (opt_gpu_path < 0)
 		opt_gpu_path = small ? XSKNF_GPU_PATH_RESIDENT : XSKNF_GPU_PATH_ZEROCOPY;
