@@ -56,14 +56,14 @@ $(VETH): tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c $(RTLIB) oracle
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ tools/xsk_veth.c xsknf_amd/csrc/rt_netlink.c \
 		-L$(LIBDIR) -lxsknf -Loracle/build -lcsum_oracle \
-		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread
+		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread -ldl
 
 # NF-level rate of the worker loop with the GPU hook (one-call / two-phase) or the CPU NF
 $(HOOKBENCH): tools/hook_bench.c $(RTLIB) $(LIB) oracle
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ tools/hook_bench.c \
 		-L$(LIBDIR) -lxsknf -lxsknf_gpu -Loracle/build -lcsum_oracle \
-		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread
+		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -pthread -ldl
 
 $(CTXLAT): tools/ctx_latency.c $(LIB)
 	@mkdir -p $(dir $@)

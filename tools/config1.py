@@ -10,9 +10,11 @@ BASELINE.json configs[0] / SURVEY.md 8(d) row 1.  Drives tools/build/xsk_veth
            REDIRECT; the frames that come back must equal the oracle's output
            byte for byte, in order
 
-The NF here is the reference per-frame path (the CPU oracle linked as
-xsknf_packet_processor): this is the CPU reference configuration, run on the
-runtime of include/xsknf.h.  Needs root (netns, XDP, AF_XDP); the GPU box
+The NF here is the reference per-frame path: the reference's own
+xsknf_packet_processor() compiled from its verbatim lines (oracle/_ref, where
+built; else the CPU restatement pinned to it; the harness's "nf" field says
+which): this is the CPU reference configuration, run on the runtime of
+include/xsknf.h.  Needs root (netns, XDP, AF_XDP); the GPU box
 runs commands unprivileged, so this runs in the build container only.
 """
 from __future__ import annotations

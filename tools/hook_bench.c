@@ -1,7 +1,10 @@
 // hook_bench.c -- frames per second through the whole NF worker loop
 // (libxsknf's worker on an emulated queue, src/xsknf.c:716-742 in shape) with
 // the checksummer as
-//   cpu    the reference per-frame NF (the CPU restatement, one worker core),
+//   cpu    the reference per-frame NF on one worker core: the reference's own
+//          xsknf_packet_processor() compiled from its verbatim lines
+//          (oracle/_ref/libcsum_ref.so, loaded at run time) where that library
+//          was built, else the CPU restatement ("cpu_nf" in the output says which),
 //   sync   the GPU hook, one batch at a time (xsknf_gpu_hook_process),
 //   async  the GPU hook, two-phase (xsknf_gpu_hook_submit / _complete: the
 //          worker receives batch k+1 while the GPU checksums batch k),
@@ -27,6 +30,7 @@
 // NF of mode "cpu" (the reference path, as tools/config1.py does).
 #define _GNU_SOURCE
 #include <arpa/inet.h>
+#include <dlfcn.h>
 #include <pthread.h>
 #include <sched.h>
 #include <stdint.h>
@@ -40,6 +44,24 @@
 
 void oracle_nf_set_options(int32_t csum_iterations, int32_t action, uint32_t num_interfaces);
 int oracle_nf_packet_processor(void *pkt, unsigned len, unsigned ingress_ifindex);
+
+// The reference's own per-packet function, if oracle/_ref was built (next to this binary's tree).
+static xsknf_packet_processor_fn load_reference_nf(const char *argv0)
+{
+	char path[4096];
+	const char *slash = strrchr(argv0, '/');
+	const int dir = slash ? (int)(slash - argv0) : 1;
+	snprintf(path, sizeof(path), "%.*s/../../oracle/_ref/libcsum_ref.so", dir, slash ? argv0 : ".");
+	void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+	if (!h)
+		return NULL;
+	void (*set)(int, int, unsigned) = (void (*)(int, int, unsigned))dlsym(h, "ref_set_options");
+	xsknf_packet_processor_fn fn = (xsknf_packet_processor_fn)dlsym(h, "xsknf_packet_processor");
+	if (!set || !fn)
+		return NULL;
+	set(1, 0, 1);   // -i 1, -c REDIRECT, one interface: the options the GPU modes run with
+	return fn;
+}
 
 static int null_nf(void *pkt, unsigned len, unsigned ingress)
 {
@@ -114,9 +136,17 @@ int main(int argc, char **argv)
 	}
 	struct xsknf_gpu_hook *hook = NULL;
 	const struct xsknf_csum_opts opts = {1, XSKNF_CSUM_ACTION_REDIRECT, 1, 0};
+	const char *cpu_nf = "none";
 	if (!strcmp(mode, "cpu")) {
-		oracle_nf_set_options(1, 0, 1);
-		xsknf_set_packet_processor(oracle_nf_packet_processor);
+		xsknf_packet_processor_fn ref = load_reference_nf(argv[0]);
+		if (ref) {
+			cpu_nf = "reference";
+			xsknf_set_packet_processor(ref);
+		} else {
+			cpu_nf = "port";
+			oracle_nf_set_options(1, 0, 1);
+			xsknf_set_packet_processor(oracle_nf_packet_processor);
+		}
 	} else if (!strcmp(mode, "null")) {
 		xsknf_set_packet_processor(null_nf);
 	} else {
@@ -213,11 +243,12 @@ int main(int argc, char **argv)
 	xsknf_cleanup();
 	const double mpps = rx / (t1 - tm) / 1e6;
 	printf("{\"checks\": \"%s\", \"mode\": \"%s\", \"len\": %u, \"batch\": %u, \"path\": \"%s\", \"depth\": %u, "
-	       "\"seconds\": %.2f, \"mpps\": %.3f, \"gbps\": %.2f, \"feeder_cpu\": %d, \"worker_error\": %d}\n",
+	       "\"seconds\": %.2f, \"mpps\": %.3f, \"gbps\": %.2f, \"feeder_cpu\": %d, \"cpu_nf\": \"%s\", "
+	       "\"worker_error\": %d}\n",
 	       nic ? "nic" : "random", mode, len, batch,
 	       path == XSKNF_GPU_PATH_STAGED ? "STAGED" : path == XSKNF_GPU_PATH_RESIDENT ? "RESIDENT" : "ZEROCOPY",
 	       depth, t1 - tm, mpps,
-	       mpps * len / 1e3, feeder_cpu, err);
+	       mpps * len / 1e3, feeder_cpu, cpu_nf, err);
 	free(frames);
 	free(txbuf);
 	return err ? 1 : 0;

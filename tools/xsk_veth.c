@@ -1,7 +1,10 @@
 // xsk_veth.c -- config 1 harness: the checksummer NF over a veth pair.
 //
-// Measurement / test infrastructure (links the CPU oracle as the per-frame
-// NF, i.e. the reference path).  Everything runs inside a private network
+// Measurement / test infrastructure.  The per-frame NF is the reference's own
+// xsknf_packet_processor() compiled from its verbatim lines
+// (oracle/_ref/libcsum_ref.so, loaded at run time) where that library was
+// built, else the CPU restatement it is pinned to ("nf" in the output says
+// which); the two-phase mode uses the restatement's batch hook.  Everything runs inside a private network
 // namespace created here (unshare), so nothing outside this process is
 // touched: veth pair xg0 <-> xn0, the xsknf runtime (include/xsknf.h) on xn0
 // in XDP skb mode (-S, hence copy mode), AF_PACKET generators on xg0.
@@ -20,6 +23,7 @@
 #define _GNU_SOURCE
 
 #include <arpa/inet.h>
+#include <dlfcn.h>
 #include <errno.h>
 #include <linux/if_ether.h>
 #include <linux/if_link.h>
@@ -336,10 +340,26 @@ int main(int argc, char **argv)
 	cfg.xsk_frame_size = 4096;
 	cfg.poll = use_poll;
 	oracle_nf_set_options(iterations, action_drop, 1);
-	if (two_phase)   // the NF as a two-phase batch hook: batches in flight across worker passes
+	const char *nf = "port";
+	if (two_phase) {   // the NF as a two-phase batch hook: batches in flight across worker passes
 		xsknf_set_batch_processor_async(oracle_nf_batch_submit, oracle_nf_batch_complete, NULL);
-	else
-		xsknf_set_packet_processor(oracle_nf_packet_processor);
+	} else {
+		// the reference's function where oracle/_ref was built, beside this binary's tree
+		char path[4096];
+		const char *slash = strrchr(argv[0], '/');
+		snprintf(path, sizeof(path), "%.*s/../../oracle/_ref/libcsum_ref.so", slash ? (int)(slash - argv[0]) : 1,
+		         slash ? argv[0] : ".");
+		void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+		void (*set)(int, int, unsigned) = h ? (void (*)(int, int, unsigned))dlsym(h, "ref_set_options") : NULL;
+		xsknf_packet_processor_fn ref = h ? (xsknf_packet_processor_fn)dlsym(h, "xsknf_packet_processor") : NULL;
+		if (set && ref) {
+			set(iterations, action_drop, 1);
+			xsknf_set_packet_processor(ref);
+			nf = "reference";
+		} else {
+			xsknf_set_packet_processor(oracle_nf_packet_processor);
+		}
+	}
 	// worker on the first CPU of our set, generators on the next ones
 	cpu_set_t set;
 	pthread_getaffinity_np(pthread_self(), sizeof(set), &set);
@@ -370,10 +390,10 @@ int main(int argc, char **argv)
 		struct xsknf_socket_stats st;
 		xsknf_get_socket_stats(0, 0, &st);
 		xsknf_cleanup();
-		printf("{\"mode\": \"check\", \"sent\": %u, \"returned\": %lu, \"rx_npkts\": %lu, "
+		printf("{\"mode\": \"check\", \"nf\": \"%s\", \"sent\": %u, \"returned\": %lu, \"rx_npkts\": %lu, "
 		       "\"tx_npkts\": %lu, \"rx_dropped\": %lu, \"tx_invalid\": %lu, \"worker_error\": %d, "
 		       "\"rc\": %d}\n",
-		       fr.n, got, st.rx_npkts, st.tx_npkts, st.rx_dropped_npkts, st.tx_invalid_npkts, werr, rc);
+		       nf, fr.n, got, st.rx_npkts, st.tx_npkts, st.rx_dropped_npkts, st.tx_invalid_npkts, werr, rc);
 		return rc || werr ? 1 : 0;
 	}
 
@@ -423,13 +443,13 @@ int main(int argc, char **argv)
 	struct xsknf_socket_stats st;
 	xsknf_get_socket_stats(0, 0, &st);
 	xsknf_cleanup();
-	printf("{\"mode\": \"search\", \"zero_loss_mpps\": %.4f, \"achieved_mpps\": %.4f, "
+	printf("{\"mode\": \"search\", \"nf\": \"%s\", \"zero_loss_mpps\": %.4f, \"achieved_mpps\": %.4f, "
 	       "\"generator_bound\": %s, "
 	       "\"offered_at_max_mpps\": %.4f, \"loss_at_max\": %.5f, \"trials\": %d, "
 	       "\"generators\": %d, \"nf_cpu\": %d, \"iterations\": %d, \"batch\": %d, "
 	       "\"rx_npkts\": %lu, \"rx_dropped\": %lu, \"rx_full\": %lu, \"fill_empty\": %lu, "
 	       "\"worker_error\": %d}\n",
-	       best, best_ach / 1e6, gen_bound ? "true" : "false", top_ach / 1e6, top_loss, trials, gen_threads, nf_cpu, iterations,
+	       nf, best, best_ach / 1e6, gen_bound ? "true" : "false", top_ach / 1e6, top_loss, trials, gen_threads, nf_cpu, iterations,
 	       batch, st.rx_npkts, st.rx_dropped_npkts, st.rx_full_npkts, st.rx_fill_empty_npkts, werr);
 	return werr ? 1 : 0;
 }
