@@ -699,6 +699,38 @@ __device__ __forceinline__ void load_lane(const FrameRef &r, uint4 (&v)[NCH]) {
   }
 }
 
+// Transposed window load (the lane kernel's TL shapes): the NCH chunks of the
+// step's 64 frames as NCH instructions whose lanes walk the frames' windows in
+// order -- lanes NCH*i .. NCH*i+NCH-1 read frame i's window, one coalesced
+// request per frame -- instead of NCH instructions that each send a 16-byte
+// request to every frame.  x[p] holds chunk (64 p + lane) % NCH of frame
+// (64 p + lane) / NCH; store_lane_tl drops it into that frame's LDS slot.
+template <int NCH>
+__device__ __forceinline__ void load_lane_tl(const FrameRef &r, uint4 (&x)[NCH]) {
+  const int lane = lane_id();
+  const uintptr_t cpv = reinterpret_cast<uintptr_t>(r.cp);
+#pragma unroll
+  for (int p = 0; p < NCH; ++p) {
+    const int j = kWave * p + lane;
+    const int f = j / NCH, c = j % NCH;
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(f << 2, static_cast<int>(cpv)));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(f << 2, static_cast<int>(cpv >> 32)));
+    const int nc = __builtin_amdgcn_ds_bpermute(f << 2, r.nch);
+    const uint4 *cp = reinterpret_cast<const uint4 *>((static_cast<uintptr_t>(hi) << 32) | lo);
+    x[p] = *XSKNF_GLD(cp + min(c, nc - 1), 16);
+  }
+}
+
+template <int NCH>
+__device__ __forceinline__ void store_lane_tl(uint32_t area, const uint4 (&x)[NCH]) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int p = 0; p < NCH; ++p) {
+    const int j = kWave * p + lane;
+    lds_store_u128(area + kLaneSlot * (j / NCH) + 16 * (j % NCH), x[p]);
+  }
+}
+
 // A lane's result; when `sector` is set, the frame's patched 64-byte check
 // sector sits in the lane's LDS slot at `lds_sec`, to be written to `gsec` by
 // the wave's cooperative store (store_sectors).
@@ -709,13 +741,16 @@ struct LaneOut {
   uint8_t *gsec;
 };
 
-template <int NCH>
+// kInSlot: the window is already in the lane's slot (transposed load), v holds a copy
+template <int NCH, bool kInSlot = false>
 __device__ __forceinline__ LaneOut process_lane(const KernelArgs &args, const FrameRef &r, const uint4 (&v)[NCH],
                                                 uint32_t slot) {
   static_assert(NCH >= 4 && NCH <= kHdrChunks, "lane window");
   LaneOut out = {0, false, slot, r.fp};
+  if constexpr (!kInSlot) {
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) lds_store_u128(slot + 16 * k, v[k]);
+    for (int k = 0; k < NCH; ++k) lds_store_u128(slot + 16 * k, v[k]);
+  }
   const int need = min(kHdrChunks, r.nch);   // header bytes past the window (large ihl)
   for (int k = NCH; k < need; ++k) lds_store_u128(slot + 16 * k, *XSKNF_GLD(r.cp + k, 16));
   compiler_barrier();
@@ -799,7 +834,13 @@ constexpr uint32_t kNoTile = 0xffffffffu;   // no tile / unit
 // block index, are a pool its waves claim from through an LDS counter, one
 // tile ahead, as the split kernel's pool (a CU's waves do not stream equally
 // fast; from a shared pool the faster ones take more tiles).
-template <int NCH, int SPT, int SW = kWavesPerBlock, int WPE = 1>
+// TLM: 0 = every lane loads its own frame's window (load_lane), 1 = transposed
+// window loads (load_lane_tl), 2 = per tile: transposed when the tile's frames
+// lie apart (a 2 KiB-chunk UMEM, or frames in fill-ring order: one coalesced
+// request per frame instead of NCH), per lane when they are packed back to
+// back (the -u layout: the lanes' own loads already stream, and the transposed
+// path's LDS round trip costs more than it saves).
+template <int NCH, int SPT, int SW = kWavesPerBlock, int WPE = 1, int TLM = 0>
 __global__ __launch_bounds__(SW * kWave) __attribute__((amdgpu_waves_per_eu(WPE)))
 void checksum_kernel_lane(const KernelArgs args) {
   constexpr uint32_t T = SPT * kWave;        // frames per tile
@@ -849,15 +890,41 @@ void checksum_kernel_lane(const KernelArgs args) {
     uint4 v[2][NCH];
     FrameRef r[2];
     r[0] = lane_ref(args, d[0], tf0 + lane);
-    load_lane<NCH>(r[0], v[0]);
+    bool tl = TLM == 1;
+    if constexpr (TLM == 2) {
+      // the tile's first and last frames' offsets: 64 frames packed back to back
+      // span a few KiB, 64 chunks of a 2 KiB-chunk UMEM 126 KiB
+      const uint64_t off = reinterpret_cast<uintptr_t>(r[0].fp) - reinterpret_cast<uintptr_t>(args.umem);
+      const uint64_t o0 = static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<int>(off), 0)) |
+                          static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<int>(off >> 32), 0)) << 32;
+      const uint64_t o1 = static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<int>(off), kWave - 1)) |
+                          static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<int>(off >> 32), kWave - 1)) << 32;
+      tl = (o1 > o0 ? o1 - o0 : o0 - o1) >= static_cast<uint64_t>(kWave - 1) * 256;
+    }
+    if (tl) load_lane_tl<NCH>(r[0], v[0]); else load_lane<NCH>(r[0], v[0]);
 #pragma unroll
     for (int st = 0; st < SPT; ++st) {
       // step st: process buffer st & 1, prefetch step st + 1 into the other
       if (st + 1 < SPT) {
         r[(st + 1) & 1] = lane_ref(args, d[st + 1], tf0 + (st + 1) * kWave + lane);
-        load_lane<NCH>(r[(st + 1) & 1], v[(st + 1) & 1]);
+        if (tl) load_lane_tl<NCH>(r[(st + 1) & 1], v[(st + 1) & 1]);
+        else load_lane<NCH>(r[(st + 1) & 1], v[(st + 1) & 1]);
       }
-      const LaneOut o = process_lane<NCH>(args, r[st & 1], v[st & 1], slot);
+      LaneOut o;
+      if (tl) {
+        // the step's windows into their frames' slots (the previous step's
+        // reads of the slots are done: a wave's LDS operations stay in order),
+        // then each lane reads its own frame's back
+        compiler_barrier();
+        store_lane_tl<NCH>(lds_addr(&hdr[wv][0][0]), v[st & 1]);
+        compiler_barrier();
+        uint4 own[NCH];
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) own[k] = lds_u128(slot + 16 * k);
+        o = process_lane<NCH, true>(args, r[st & 1], own, slot);
+      } else {
+        o = process_lane<NCH>(args, r[st & 1], v[st & 1], slot);
+      }
       store_sectors(o, lane, args.plain_sector);
       const uint32_t f = tf0 + st * kWave + lane;
       nrec += store_result(args, f, f < args.n, o.res);
@@ -2401,9 +2468,9 @@ int launch_reg(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel launch");
 }
 
-template <int NCH, int SPT, int SW = kWavesPerBlock, int WPE = 1>
+template <int NCH, int SPT, int SW = kWavesPerBlock, int WPE = 1, int TLM = 0>
 int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  auto k = checksum_kernel_lane<NCH, SPT, SW, WPE>;
+  auto k = checksum_kernel_lane<NCH, SPT, SW, WPE, TLM>;
   if constexpr (SW > kWavesPerBlock) {   // as launch_split: a CU-sized block the device cannot hold
     static thread_local int fits = -1;
     if (fits < 0) {
@@ -2487,6 +2554,10 @@ struct Variant {
 #define XSKNF_L(N, S) {1, N, S, 0, &launch_lane<N, S>}
 // lane kernel, one 16-wave block per CU with the tile pool (window field 32)
 #define XSKNF_LP(N, S) {1, N, S, 0, &launch_lane<N, S, 16>, XSKNF_GPU_KERNEL_AUTO, 32}
+// lane kernel with the transposed (coalesced) window load (window field 512)
+#define XSKNF_LT(N, S) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, 1, 1>, XSKNF_GPU_KERNEL_AUTO, 512}
+// ... transposed per tile where the tile's frames lie apart (window field 1024)
+#define XSKNF_LA(N, S) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, 4, 2>, XSKNF_GPU_KERNEL_AUTO, 1024}
 // (A/B) lane kernel held to WPE waves per SIMD (window field 64 + 256 * WPE)
 #define XSKNF_LW(N, S, WPE) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, WPE>, XSKNF_GPU_KERNEL_AUTO, 64 + 256 * WPE}
 #define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
@@ -2520,6 +2591,9 @@ const Variant kVariants[] = {
     XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
     XSKNF_SC4W(16, 3, 2), XSKNF_SC(16, 2, 3),
     XSKNF_LP(5, 2),   // lane kernel with the tile pool: 64 B 59.65 vs 59.51 us, a tie (r02 ab_pool_lane.jsonl)
+    // transposed window loads (r04 ab_lane_transposed*.jsonl): aligned 64 B NIC -1 us, worst case +0.3,
+    // packed (-u) frames +1 us; per tile by the frames' spread: worst case +2 us (4 waves per SIMD forced)
+    XSKNF_LT(5, 2), XSKNF_LT(4, 2), XSKNF_LT(5, 1), XSKNF_LA(5, 2), XSKNF_LA(5, 1),
     XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
     XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
     XSKNF_SP(16, 2, 2), XSKNF_SP(16, 3, 1),         // window prefetch: +3-6 us on 1500 / IMIX / 570 (tune_pfw)
@@ -2543,6 +2617,8 @@ const Variant kVariants[] = {
 #undef XSKNF_V
 #undef XSKNF_L
 #undef XSKNF_LP
+#undef XSKNF_LT
+#undef XSKNF_LA
 #undef XSKNF_LW
 #undef XSKNF_D
 #undef XSKNF_S
