@@ -728,8 +728,8 @@ def test_resident_rings_past_the_device_limit_are_refused(dev):
     umems = [b.umem.copy() for b in bs]
     hps = []
     try:
-        for u in umems:
-            hps.append(HostPath(cs, u, path="resident", max_batch=512))
+        for k, u in enumerate(umems):   # (one- and four-block groups: both fit at 8 entries per block)
+            hps.append(HostPath(cs, u, path="resident", max_batch=64 if k % 4 else 512))
         extra = np.zeros(4096, dtype=np.uint8)
         with pytest.raises(XsknfGpuError, match="rc=-28"):
             HostPath(cs, extra, path="resident", max_batch=64)
