@@ -1270,8 +1270,19 @@ constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with 
 // Tiles in a wave's patch list: 16 x 2 items fit 3 waves per SIMD (6 tiles per
 // wave at 1M frames; 7 with the pool, whose faster waves take more units), 16 x
 // 3 fit 2 (8 tiles per wave); the other shapes keep no list.
+// The compact shape (A/B: W = 8, 16 x 2, one item in flight, 4-wave blocks)
+// fits 4 waves per SIMD by registers (<= 128 VGPRs) and 4 blocks per CU by
+// LDS: its phase-B scratch (item queue, frame meta, accumulators) lives in the
+// wave's window slots, dead once phase A has read them (every check deferred),
+// and its list holds 4 tiles (4 x 64 x 8 B): 40 KiB per block.
+template <int W, int NCH, int U, bool DMA, bool PFW, bool kPool>
+constexpr bool compact_split() {
+  return W == 8 && NCH == 2 && U == 1 && !DMA && !PFW && !kPool;
+}
+
 template <int W, int NCH, int U, bool DMA, bool PFW, bool kPool>
 constexpr int patch_list_tiles() {
+  if constexpr (compact_split<W, NCH, U, DMA, PFW, kPool>()) return 4;
   return (W == 8 && U >= 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
 }
 
@@ -1389,11 +1400,13 @@ void checksum_kernel_split(const KernelArgs args) {
   constexpr int kSlotArea = kWave * kSlot;                 // bytes per wave
   constexpr int kItemCap = 256;                            // items per round of phase B
   constexpr uint32_t kItemsPerFrame = 255;                 // u8 pass index; more: whole-wave loop
-  __shared__ __attribute__((aligned(16))) uint8_t slots[SW][kSlotArea];
-  __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kItemCap];
-  __shared__ __attribute__((aligned(16))) uint4 meta[SW][kWave];
-  __shared__ __attribute__((aligned(16))) uint32_t accb[SW][kWave];
   constexpr bool kPool = SW > kWavesPerBlock;   // one block per CU: its waves share the CU's tiles
+  constexpr bool kCompact = compact_split<W, NCH, U, DMA, PFW, kPool>();
+  constexpr int kScratch = kCompact ? 1 : kWave;   // phase-B scratch of its own (else in the slots)
+  __shared__ __attribute__((aligned(16))) uint8_t slots[SW][kSlotArea];
+  __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kCompact ? 1 : kItemCap];
+  __shared__ __attribute__((aligned(16))) uint4 meta[SW][kScratch];
+  __shared__ __attribute__((aligned(16))) uint32_t accb[SW][kScratch];
   // (jumbo keeps no list: with the pool and a 16-unit list, patching after the last unit tied the
   // scatter pass, 1463 vs 1461 us -- profiles/r02/ab_jumbo_tail.jsonl)
   constexpr int PT = patch_list_tiles<W, NCH, U, DMA, PFW, kPool>();
@@ -1404,9 +1417,10 @@ void checksum_kernel_split(const KernelArgs args) {
   const int grp = lane / LPF, gl = lane % LPF;
   const uint32_t area = lds_addr(&slots[wv][0]);
   const uint32_t slot = area + kSlot * lane;
-  const uint32_t mt = lds_addr(&meta[wv][0]);
-  const uint32_t ab = lds_addr(&accb[wv][0]);
-  const uint32_t iq = lds_addr(&itemq[wv][0]);
+  static_assert(!kCompact || 16 * kWave + 4 * kWave + 2 * kItemCap <= kSlotArea, "scratch in the slots");
+  const uint32_t mt = kCompact ? area : lds_addr(&meta[wv][0]);
+  const uint32_t ab = kCompact ? area + 16 * kWave : lds_addr(&accb[wv][0]);
+  const uint32_t iq = kCompact ? area + 20 * kWave : lds_addr(&itemq[wv][0]);
   const uint32_t waves = gridDim.x * SW;
   const uint32_t last = args.n - 1;
 
@@ -1708,8 +1722,8 @@ void checksum_kernel_split(const KernelArgs args) {
         if (static_cast<uint32_t>(r.len) >= defer_min) {
           if (to_list) ent = patch_entry(args, r, h.u, c, 16 * W);
           else res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
-        } else if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
-                   sec + 64 <= c0 + 16 * W) {
+        } else if (!kCompact && args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 &&
+                   sec >= c0 && sec + 64 <= c0 + 16 * W) {   // (kCompact: phase B's scratch is in the slots)
           const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
           lds_store_u8(at, static_cast<uint8_t>(c));
           lds_store_u8(at + 1, static_cast<uint8_t>(c >> 8));
@@ -2418,6 +2432,9 @@ int resident_blocks(const void *kernel, int threads) {
     if (cache[i].k == kernel && cache[i].dev == dev) return cache[i].blocks;
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, threads, 0) != hipSuccess || b <= 0) b = 1;
+#ifdef XSKNF_AB
+  if (getenv("XSKNF_AB_OCCUPANCY")) fprintf(stderr, "occupancy %p x %d threads: %d blocks per CU\n", kernel, threads, b);
+#endif
   if (used < 64) cache[used++] = Entry{kernel, dev, b};
   return b;
 }
