@@ -6,12 +6,16 @@
 # the pooled 12-wave shape, on IMIX (worst case and NIC checks), 570 B and
 # 1500 B; one process per workload, shapes interleaved (tools/tune.py):
 #   tools/ab_compact.sh <tag>  -> gpurun_out/<tag>/ab_compact.jsonl
+# ABC_LIB (default build/ab) and ABC_VARIANTS override the library and shapes:
+# build/ab_big (the A/B build with -DXSKNF_BIG_STATIC=1: blocks of more than 4
+# waves deal their tiles statically) adds the compact shape as one 16-wave
+# block per CU (window field 152).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/${1:-abc}
 mkdir -p "$OUT"
-V="16,2,2,0,18,1,24:16,2,1,0,18,1,24:16,2,2,0,18,1,56"
-export XSKNF_GPU_LIB=$R/build/ab/libxsknf_gpu.so
+V=${ABC_VARIANTS:-"16,2,2,0,18,1,24:16,2,1,0,18,1,24:16,2,2,0,18,1,56"}
+export XSKNF_GPU_LIB=$R/${ABC_LIB:-build/ab}/libxsknf_gpu.so
 for rep in 1 2; do
   for W in imix:zero:3 imix:nic:3 570:zero:3 1500:zero:1; do
     IFS=: read -r WL C ROT <<< "$W"

@@ -1275,6 +1275,13 @@ constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with 
 // LDS: its phase-B scratch (item queue, frame meta, accumulators) lives in the
 // wave's window slots, dead once phase A has read them (every check deferred),
 // and its list holds 4 tiles (4 x 64 x 8 B): 40 KiB per block.
+// A block of more than 4 waves holds a whole CU's waves and shares the CU's
+// tiles as a pool; XSKNF_BIG_STATIC (A/B) deals them statically instead.
+#ifndef XSKNF_BIG_STATIC
+#define XSKNF_BIG_STATIC 0
+#endif
+constexpr bool pooled_split(int sw) { return sw > kWavesPerBlock && !XSKNF_BIG_STATIC; }
+
 template <int W, int NCH, int U, bool DMA, bool PFW, bool kPool>
 constexpr bool compact_split() {
   return W == 8 && NCH == 2 && U == 1 && !DMA && !PFW && !kPool;
@@ -1400,7 +1407,7 @@ void checksum_kernel_split(const KernelArgs args) {
   constexpr int kSlotArea = kWave * kSlot;                 // bytes per wave
   constexpr int kItemCap = 256;                            // items per round of phase B
   constexpr uint32_t kItemsPerFrame = 255;                 // u8 pass index; more: whole-wave loop
-  constexpr bool kPool = SW > kWavesPerBlock;   // one block per CU: its waves share the CU's tiles
+  constexpr bool kPool = pooled_split(SW);   // one block per CU: its waves share the CU's tiles
   constexpr bool kCompact = compact_split<W, NCH, U, DMA, PFW, kPool>();
   constexpr int kScratch = kCompact ? 1 : kWave;   // phase-B scratch of its own (else in the slots)
   __shared__ __attribute__((aligned(16))) uint8_t slots[SW][kSlotArea];
@@ -2518,7 +2525,7 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
     if (!fits) return launch_split<W, LPF, NCH, U, TL, DMA, PFW, kWavesPerBlock>(a, stream, blocks_per_cu);
   }
   uint32_t grid = grid_blocks(k, a.n, blocks_per_cu, kWave, SW);
-  constexpr uint32_t PT = patch_list_tiles<W, NCH, U, DMA, PFW, (SW > kWavesPerBlock)>();
+  constexpr uint32_t PT = patch_list_tiles<W, NCH, U, DMA, PFW, pooled_split(SW)>();
   if constexpr (PT > 0) {
     // Enough blocks that every tile's check goes to a patch list, whatever
     // blocks_per_cu asks or the device's CU count (blocks past residency start
@@ -2530,7 +2537,7 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
     // not these kernels -- DESIGN 3; tested by test_no_wave_passes_its_patch_list.)
     if (a.tail_scatter) {
       const uint32_t tiles = (a.n + kWave - 1) / kWave;
-      constexpr uint32_t per_block = SW > kWavesPerBlock ? SW * (PT - 1) : SW * PT;
+      constexpr uint32_t per_block = pooled_split(SW) ? SW * (PT - 1) : SW * PT;
       const uint32_t fit = (tiles + per_block - 1) / per_block;
       if (grid < fit) grid = fit;
     }
@@ -2607,6 +2614,10 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
     XSKNF_SC4W(16, 3, 2), XSKNF_SC(16, 2, 3),
+#if XSKNF_BIG_STATIC
+    // the compact shape as one 16-wave block per CU, tiles dealt statically (window field 152)
+    {16, 2, 1, 0, &launch_split<8, 16, 2, 1, true, false, false, 16>, XSKNF_GPU_KERNEL_SPLIT, 152},
+#endif
     XSKNF_LP(5, 2),   // lane kernel with the tile pool: 64 B 59.65 vs 59.51 us, a tie (r02 ab_pool_lane.jsonl)
     // transposed window loads (r04 ab_lane_transposed*.jsonl): aligned 64 B NIC -1 us, worst case +0.3,
     // packed (-u) frames +1 us; per tile by the frames' spread: worst case +2 us (4 waves per SIMD forced)
