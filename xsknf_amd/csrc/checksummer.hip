@@ -1463,6 +1463,7 @@ void checksum_kernel_split(const KernelArgs args) {
   __shared__ uint32_t pool_next;
   const uint32_t nb = gridDim.x;
   const uint32_t bt = ntiles > blockIdx.x ? (ntiles - blockIdx.x + nb - 1) / nb : 0u;   // the block's tiles
+  const auto tile_of = [&](uint32_t k) { return blockIdx.x + k * nb; };
   // The pool's units: the block's tiles, except that its last SW tiles run as
   // kParts parts each, so the waves' streams end closer together: halves up to
   // 4 KiB (quarters there: 570 B 165 vs 151 us, 1024 B 213 vs 205 --
@@ -1479,9 +1480,9 @@ void checksum_kernel_split(const KernelArgs args) {
   // first frame and frame count of unit / static tile u
   const auto unit_f0 = [&](uint32_t u) -> uint32_t {
     if constexpr (kPool) {
-      if (u < nfull) return (blockIdx.x + u * nb) * kWave;
+      if (u < nfull) return tile_of(u) * kWave;
       const uint32_t h = u - nfull;
-      return (blockIdx.x + (nfull + h / kParts) * nb) * kWave + (h % kParts) * (kWave / kParts);
+      return tile_of(nfull + h / kParts) * kWave + (h % kParts) * (kWave / kParts);
     } else {
       return u * kWave;
     }
