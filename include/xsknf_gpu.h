@@ -215,8 +215,10 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size
  *                            that also launches work of its own (ZEROCOPY /
  *                            STAGED contexts, torch) may find a launch queued
  *                            behind it for up to those 4 ms when its streams
- *                            outnumber the hardware queues, so give such a
- *                            process one path.  Creating a context returns
+ *                            outnumber the hardware queues.  (Measured with 4
+ *                            RESIDENT and 4 ZEROCOPY workers in one process:
+ *                            no such wait, each side 10-40 % slower per batch
+ *                            than alone -- DESIGN 5.3.)  Creating a context returns
  *                            -ENOSPC past 64 rings per device.
  * One context = one worker thread.  A launched context keeps up to five batches in
  * flight (five slots, each with its own HIP stream: four out plus the one being

@@ -5,8 +5,11 @@
 // each batch waited for right after its submit: the round trip itself).
 // WORKERS (default 1) threads run the same loop at once, each with its own
 // context and UMEM, as the AF_XDP workers of src/xsknf.c:1075-1095 would (on
-// RESIDENT they share the device's one resident kernel).
-//   ctx_latency LEN N ITERS [ZEROCOPY|STAGED|RESIDENT [DEPTH [WORKERS]]]
+// RESIDENT they share the device's one resident kernel).  The path may be a
+// comma-separated list, dealt to the workers in turn (RESIDENT,ZEROCOPY: a mixed
+// set, the resident kernel's hardware queue beside the launches' streams); the
+// output then also has each path's mean per batch.
+//   ctx_latency LEN N ITERS [ZEROCOPY|STAGED|RESIDENT[,...] [DEPTH [WORKERS]]]
 #define _GNU_SOURCE
 #include <pthread.h>
 #include <stdint.h>
@@ -101,9 +104,16 @@ int main(int argc, char **argv)
 	proto.len = (unsigned)atoi(argv[1]);
 	proto.n = (unsigned)atoi(argv[2]);
 	proto.iters = (unsigned)atoi(argv[3]);
-	proto.path = argc > 4 && !strcmp(argv[4], "STAGED")     ? XSKNF_GPU_PATH_STAGED
-	             : argc > 4 && !strcmp(argv[4], "RESIDENT") ? XSKNF_GPU_PATH_RESIDENT
-	                                                        : XSKNF_GPU_PATH_ZEROCOPY;
+	int paths[8], npaths = 0;
+	char spec[128];
+	snprintf(spec, sizeof(spec), "%s", argc > 4 ? argv[4] : "ZEROCOPY");
+	for (char *t = strtok(spec, ","); t && npaths < 8; t = strtok(NULL, ","))
+		paths[npaths++] = !strcmp(t, "STAGED") ? XSKNF_GPU_PATH_STAGED
+		                  : !strcmp(t, "RESIDENT") ? XSKNF_GPU_PATH_RESIDENT
+		                                           : XSKNF_GPU_PATH_ZEROCOPY;
+	if (npaths == 0)
+		return 2;
+	proto.path = paths[0];
 	proto.depth = argc > 5 ? (unsigned)atoi(argv[5]) : 2;
 	const unsigned workers = argc > 6 ? (unsigned)atoi(argv[6]) : 1;
 	if (proto.depth < 1 || proto.depth > 8 || proto.iters <= 16 || workers < 1 || workers > 64)
@@ -114,15 +124,21 @@ int main(int argc, char **argv)
 	pthread_t tid[64];
 	for (unsigned i = 0; i < workers; i++) {
 		w[i] = proto;
+		w[i].path = paths[i % npaths];
 		w[i].start = &start;
 		if (pthread_create(&tid[i], NULL, run, &w[i]))
 			return 1;
 	}
-	double per = 0, sub = 0, wait = 0, worst = 0;
+	double per = 0, sub = 0, wait = 0, worst = 0, path_us[3] = {0}, mpps = 0;
+	unsigned path_n[3] = {0};
 	int rc = 0;
 	for (unsigned i = 0; i < workers; i++) {
 		pthread_join(tid[i], NULL);
 		rc |= w[i].rc;
+		path_us[w[i].path] += w[i].us_per_batch;
+		path_n[w[i].path]++;
+		if (w[i].us_per_batch > 0)
+			mpps += proto.n / w[i].us_per_batch;
 		per += w[i].us_per_batch / workers;
 		sub += w[i].submit_us / workers;
 		wait += w[i].wait_us / workers;
@@ -133,10 +149,20 @@ int main(int argc, char **argv)
 		fprintf(stderr, "ctx_latency: a worker failed: %s\n", xsknf_gpu_last_error());
 		return 1;
 	}
+	static const char *const names[3] = {"ZEROCOPY", "STAGED", "RESIDENT"};
 	printf("{\"len\": %u, \"n\": %u, \"path\": \"%s\", \"depth\": %u, \"workers\": %u, \"us_per_batch\": %.2f, "
 	       "\"us_per_batch_worst_worker\": %.2f, \"submit_cpu_us\": %.2f, \"wait_us\": %.2f, "
-	       "\"mpps_all_workers\": %.2f}\n", proto.len, proto.n,
-	       proto.path == XSKNF_GPU_PATH_STAGED ? "STAGED" : proto.path == XSKNF_GPU_PATH_RESIDENT ? "RESIDENT" : "ZEROCOPY",
-	       proto.depth, workers, per, worst, sub, wait, workers * proto.n / per);
+	       "\"mpps_all_workers\": %.2f", proto.len, proto.n, argc > 4 ? argv[4] : "ZEROCOPY", proto.depth, workers, per,
+	       worst, sub, wait, npaths > 1 ? mpps : workers * proto.n / per);
+	if (npaths > 1) {
+		printf(", \"us_per_batch_by_path\": {");
+		for (int p = 0, first = 1; p < 3; p++)
+			if (path_n[p]) {
+				printf("%s\"%s\": %.2f", first ? "" : ", ", names[p], path_us[p] / path_n[p]);
+				first = 0;
+			}
+		printf("}");
+	}
+	printf("}\n");
 	return 0;
 }
