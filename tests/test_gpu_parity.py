@@ -716,6 +716,56 @@ def test_resident_rings_join_and_leave_under_traffic(dev):
         assert np.array_equal(umems[k], refs[k][0]), k
 
 
+def test_mixed_paths_from_worker_threads(dev):
+    """Worker threads on one device, each with its own context and UMEM as the
+    reference's workers (src/xsknf.c:1075-1095), on different host paths at
+    once: two RESIDENT (the shared kernel's hardware queue), two ZEROCOPY and
+    two STAGED (launches on their own streams), each keeping four batches out.
+    Every worker's verdicts and bytes equal the oracle's."""
+    import threading
+    from xsknf_amd import HostPath
+    paths = ["resident", "zerocopy", "staged"] * 2
+    bs = [frames.unaligned_batch(3000, "imix", seed=90 + k) for k in range(len(paths))]
+    for k, b in enumerate(bs):
+        frames.inject_edge_cases(b, 0.05, seed=100 + k)
+    refs = [run_oracle(b, iters=3, action=O.REDIRECT, nif=2, ingress=1) for b in bs]
+    cs = Checksummer(ChecksummerOptions(action=O.REDIRECT, csum_iterations=3), num_interfaces=2,
+                     frame_len_hint=1500)
+    umems = [b.umem.copy() for b in bs]
+    outs = [np.full(b.n, 7, dtype=np.int32) for b in bs]
+    errors, stats = [], [None] * len(paths)
+    start = threading.Barrier(len(paths))
+
+    def worker(k):
+        try:
+            with HostPath(cs, umems[k], path=paths[k], max_batch=64) as hp:
+                start.wait()
+                tickets = []
+                for lo in range(0, bs[k].n, 64):
+                    tickets.append(hp.submit(bs[k].descs[lo:lo + 64], outs[k][lo:lo + 64], ingress_ifindex=1))
+                    if len(tickets) >= 4:
+                        hp.wait(tickets[-4])
+                hp.wait(tickets[-1])
+                stats[k] = hp.stats()
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errors.append((k, repr(e)))
+            start.abort()
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(len(paths))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(120)
+    assert not any(t.is_alive() for t in threads), "a worker did not finish"
+    assert not errors, errors
+    for k, p in enumerate(paths):
+        assert stats[k]["frames"] == bs[k].n
+        if p == "resident":
+            assert stats[k]["resident_batches"] == sum(_entries(min(64, bs[k].n - lo)) for lo in range(0, bs[k].n, 64))
+        assert np.array_equal(outs[k], refs[k][1]), (k, p)
+        assert np.array_equal(umems[k], refs[k][0]), (k, p)
+
+
 def test_resident_rings_past_the_device_limit_are_refused(dev):
     """64 rings per device (XSKNF_MAX_WORKERS x a zero-copy and a copy-mode
     UMEM); a 65th RESIDENT context is refused with -ENOSPC instead of running
