@@ -69,6 +69,7 @@
 #include <atomic>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/xsknf_gpu.h"
@@ -375,6 +376,22 @@ void svc_remove(xsknf_gpu_ctx *c) {
   (void)svc_launch_locked(s);
 }
 
+// A context whose batch never completed: stop the kernel, give it a bounded
+// time to leave (its polls and batches are bounded by the clock), and take the
+// ring out of the table, so that no later launch -- made for the other rings --
+// reads this ring's entries again and writes into frames the caller may
+// recycle after the error.
+void svc_fail(xsknf_gpu_ctx *c) {
+  ResService &s = g_svc[c->device];
+  std::lock_guard<std::mutex> lk(s.mu);
+  svc_set_stop(s, 1);
+  for (int i = 0; i < 1000 && s.launched.load() && hipEventQuery(s.done) == hipErrorNotReady; ++i)
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  if (c->ring_idx >= 0) s.rings[c->ring_idx] = nullptr;
+  c->ring_idx = -1;
+  // the other rings: their next submit or wait relaunches the kernel (svc_ensure)
+}
+
 void release(xsknf_gpu_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
@@ -458,10 +475,9 @@ int ring_complete(xsknf_gpu_ctx *c, RingEntry &r) {
         if (q != hipSuccess && q != hipErrorNotReady) return fail(q, "resident kernel");
         if (t - t0 > 10.0) {
           // every launch lives at most a few ms and is relaunched on demand:
-          // something is wrong.  Stop the kernel so that it writes nothing more
-          // into frames the caller may recycle after this error, and fail every
-          // later call of this context at once.
-          svc_set_stop(s, 1);
+          // something is wrong.  Stop the kernel and take the ring out of its
+          // table (svc_fail), and fail every later call of this context at once.
+          svc_fail(c);
           c->failed = -ETIMEDOUT;
           xsknf_gpu::set_error_text("resident kernel: no completion within 10 s");
           return -ETIMEDOUT;
