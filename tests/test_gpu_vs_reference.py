@@ -91,3 +91,42 @@ def test_host_paths_equal_the_reference(dev, path):
         v = np.concatenate([hp.process_batch(b.descs[lo:lo + 500], ingress_ifindex=1) for lo in range(0, b.n, 500)])
     assert np.array_equal(v, rv)
     assert np.array_equal(umem, ref.umem)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_sweep_equals_the_reference(dev, seed):
+    """Randomized cases against the reference's function, one per seed: frame
+    count, longest frame (0 .. 9100 B: every launch family the hint picks),
+    layout, the hint given (right, 0 = unknown, or too small: a hint is only a
+    hint), the mean given or not, iterations -3 .. 7919, action, 1-4
+    interfaces, ingress, and half of the batches with NIC-offloaded checks (the
+    kernels' write elision) before the edge cases."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(1, 6000))
+    max_len = int(rng.choice([64, 128, 200, 600, 1500, 1792, 4000, 9100]))
+    layout = "aligned" if max_len <= 1792 and rng.random() < 0.5 else "unaligned"
+    lens = rng.integers(0, max_len + 1, size=n).astype(np.uint32)
+    if layout == "aligned":
+        b = frames.aligned_batch(n, lens, seed=seed)
+    else:
+        b = frames.unaligned_batch(n, lens, seed=seed)
+    if rng.random() < 0.5:
+        frames.offload_checks_host(b)
+    frames.inject_edge_cases(b, float(rng.uniform(0.02, 0.3)), seed=seed + 7)
+    it = int(rng.choice([-3, 0, 1, 2, 3, 5, 17, 255, 7919]))
+    act, nif, ing = int(rng.integers(0, 2)), int(rng.integers(1, 5)), int(rng.integers(0, 6))
+    hint = int(rng.choice([0, max_len, max(1, max_len // 3)]))
+    mean = int(b.descs["len"].mean()) if rng.random() < 0.5 else 0
+    ref = b.copy()
+    rv = R.process_batch(ref.umem, ref.descs, ingress=ing, iters=it, action=act, nif=nif)
+    cs = Checksummer(ChecksummerOptions(action=act, csum_iterations=it), num_interfaces=nif,
+                     frame_len_hint=hint, frame_len_mean=mean)
+    umem = torch.from_numpy(b.umem).to(dev)
+    descs = torch.from_numpy(b.descs.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+    v = cs.process_batch(umem, descs, ingress_ifindex=ing)
+    torch.cuda.synchronize()
+    gv, gu = v.cpu().numpy(), umem.cpu().numpy()
+    bad = np.nonzero(gv != rv)[0]
+    assert bad.size == 0, f"verdicts differ at {bad[:8]}: gpu {gv[bad[:8]]} reference {rv[bad[:8]]}"
+    diff = np.nonzero(gu != ref.umem)[0]
+    assert diff.size == 0, f"{diff.size} UMEM bytes differ, first at {diff[:8]}"
