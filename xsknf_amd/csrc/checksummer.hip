@@ -1410,6 +1410,13 @@ void checksum_kernel_split(const KernelArgs args) {
   constexpr bool kPool = pooled_split(SW);   // one block per CU: its waves share the CU's tiles
   constexpr bool kCompact = compact_split<W, NCH, U, DMA, PFW, kPool>();
   constexpr int kScratch = kCompact ? 1 : kWave;   // phase-B scratch of its own (else in the slots)
+  // Phase C's in-line sector stores take the sector from the lane's window
+  // slot, which phase B has overwritten where it keeps its stages (DMA), the
+  // next tile's windows (PFW) or its scratch (kCompact) there: those shapes
+  // store a phase-C check as its 2 bytes.  (With every check deferred they
+  // store none in-line, except past the patch list -- the DMA and PFW shapes
+  // keep no list, so with tail patches asked for all of theirs are in-line.)
+  constexpr bool kSlotsLiveInC = !kCompact && !DMA && !PFW;
   __shared__ __attribute__((aligned(16))) uint8_t slots[SW][kSlotArea];
   __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kCompact ? 1 : kItemCap];
   __shared__ __attribute__((aligned(16))) uint4 meta[SW][kScratch];
@@ -1504,6 +1511,38 @@ void checksum_kernel_split(const KernelArgs args) {
     tile = t0 < ntiles ? t0 : kNoTile;
     tn = t0 + waves < ntiles ? t0 + waves : kNoTile;
     tnn = t0 + 2 * waves < ntiles ? t0 + 2 * waves : kNoTile;
+  }
+#ifndef XSKNF_PATCH_SHARED
+#define XSKNF_PATCH_SHARED 0
+#endif
+  // (A/B) One patch queue per block instead of each wave patching its own list
+  // after its last unit: a wave publishes each finished unit's list (its index,
+  // or a null mark for a unit with nothing to patch), and a wave whose stream
+  // is done takes the next published unit of ANY wave of the block, so the
+  // block's last stream is followed by one unit's patches, not by its wave's
+  // whole list.  Every wave publishes one mark per unit; the block's count of
+  // units is known, so the consumers' loop ends; the wait for a mark is bounded
+  // by the clock.
+  constexpr bool kShared = XSKNF_PATCH_SHARED && PT > 0;
+  constexpr uint32_t kPQ = kShared ? SW * PT : 1;   // marks: the grid is sized so a block has <= SW * PT units
+  constexpr uint32_t kPQNull = 0xffffu;
+  __shared__ uint32_t pq_tail, pq_head;
+  __shared__ uint32_t pq[kPQ];
+  const bool shared_on = kShared && list_ok;   // block-uniform
+  bool pq_full = false;                        // wave-uniform: a mark found no room
+  uint32_t block_units = 0;
+  if constexpr (kShared) {
+    if constexpr (kPool) {
+      block_units = units;
+    } else {
+      for (int w = 0; w < SW; ++w) {
+        const uint32_t t0 = blockIdx.x * SW + w;
+        block_units += t0 < ntiles ? (ntiles - t0 + waves - 1) / waves : 0u;
+      }
+    }
+    if (threadIdx.x == 0) pq_tail = pq_head = 0;
+    for (uint32_t i = threadIdx.x; i < kPQ; i += SW * kWave) pq[i] = 0;
+    __syncthreads();
   }
   const auto desc_of = [&](uint32_t t) {
     return *XSKNF_GLD(reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(unit_f0(t) + lane, last))), 16);
@@ -1730,8 +1769,8 @@ void checksum_kernel_split(const KernelArgs args) {
         if (static_cast<uint32_t>(r.len) >= defer_min) {
           if (to_list) ent = patch_entry(args, r, h.u, c, 16 * W);
           else res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
-        } else if (!kCompact && args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 &&
-                   sec >= c0 && sec + 64 <= c0 + 16 * W) {   // (kCompact: phase B's scratch is in the slots)
+        } else if (kSlotsLiveInC && args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 &&
+                   sec >= c0 && sec + 64 <= c0 + 16 * W) {
           const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
           lds_store_u8(at, static_cast<uint8_t>(c));
           lds_store_u8(at + 1, static_cast<uint8_t>(c >> 8));
@@ -1749,6 +1788,22 @@ void checksum_kernel_split(const KernelArgs args) {
     if (to_list) {
       lds_store_u64(pl + 8 * (it * kWave + lane), ent);
       any_entry |= __builtin_amdgcn_ballot_w64(ent.y != 0) != 0;
+    }
+    if constexpr (kShared) {
+      if (shared_on) {   // publish this unit's list (the entries are in LDS before the mark)
+        const bool tany = to_list && __builtin_amdgcn_ballot_w64(ent.y != 0) != 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint32_t slot = 0;
+        if (lane == 0) slot = __hip_atomic_fetch_add(&pq_tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        slot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(slot), 0));
+        if (slot < kPQ) {
+          if (lane == 0)
+            __hip_atomic_store(&pq[slot], tany ? (static_cast<uint32_t>(wv) << 8 | static_cast<uint32_t>(it)) + 1u : kPQNull,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          pq_full = true;   // (never: the grid is sized) the wave patches its whole list itself at the end
+        }
+      }
     }
     ++it;
     compiler_barrier();   // the next tile rewrites the slots
@@ -1769,7 +1824,29 @@ void checksum_kernel_split(const KernelArgs args) {
   const unsigned long long tl1 = wall_clock64();
 #endif
   if (args.tail_scatter) {
-    if (any_entry) tail_patch_list(args, pl, min(it, PT), lane, it <= PT, area, kSlot);
+    if constexpr (kShared) {
+      if (shared_on) {
+        const uint64_t tw0 = wall_clock64();
+        for (;;) {
+          uint32_t h = 0;
+          if (lane == 0) h = __hip_atomic_fetch_add(&pq_head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          h = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(h), 0));
+          if (h >= block_units || h >= kPQ) break;
+          uint32_t m = 0;
+          for (;;) {
+            m = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
+                __hip_atomic_load(&pq[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))));
+            if (m != 0 || wall_clock64() - tw0 > 2000000ull) break;   // 20 ms: never, unless units went unclaimed
+            __builtin_amdgcn_s_sleep(2);
+          }
+          if (m == 0) break;
+          if (m != kPQNull)
+            tail_patch_list(args, lds_addr(&plist[(m - 1) >> 8][0]) + 8 * ((m - 1) & 0xffu) * kWave, 1, lane, false,
+                            area, kSlot);
+        }
+      }
+    }
+    if (any_entry && (!shared_on || pq_full)) tail_patch_list(args, pl, min(it, PT), lane, it <= PT, area, kSlot);
 #ifdef XSKNF_RECORD_PATH
     if (!kPool && __builtin_amdgcn_readfirstlane(nrec))
       tail_scatter(args, blockIdx.x * SW + wv + (list_ok ? PT : 0) * waves, waves, lane);
