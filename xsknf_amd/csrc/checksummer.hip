@@ -1523,7 +1523,7 @@ void checksum_kernel_split(const KernelArgs args) {
   // whole list.  Every wave publishes one mark per unit; the block's count of
   // units is known, so the consumers' loop ends; the wait for a mark is bounded
   // by the clock.
-  constexpr bool kShared = XSKNF_PATCH_SHARED && PT > 0;
+  constexpr bool kShared = XSKNF_PATCH_SHARED && PT > 0 && kPool;   // (static 4-wave IMIX: +1 us)
   constexpr uint32_t kPQ = kShared ? SW * PT : 1;   // marks: the grid is sized so a block has <= SW * PT units
   constexpr uint32_t kPQNull = 0xffffu;
   __shared__ uint32_t pq_tail, pq_head;
