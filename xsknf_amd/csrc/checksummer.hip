@@ -1528,6 +1528,7 @@ void checksum_kernel_split(const KernelArgs args) {
   constexpr uint32_t kPQNull = 0xffffu;
   __shared__ uint32_t pq_tail, pq_head;
   __shared__ uint32_t pq[kPQ];
+  __shared__ uint32_t pq_last[kShared ? SW : 1];   // a wave's last unit, once it has no more (its slots hold it)
   const bool shared_on = kShared && list_ok;   // block-uniform
   bool pq_full = false;                        // wave-uniform: a mark found no room
   uint32_t block_units = 0;
@@ -1542,6 +1543,7 @@ void checksum_kernel_split(const KernelArgs args) {
     }
     if (threadIdx.x == 0) pq_tail = pq_head = 0;
     for (uint32_t i = threadIdx.x; i < kPQ; i += SW * kWave) pq[i] = 0;
+    if (threadIdx.x < SW) pq_last[threadIdx.x] = ~0u;
     __syncthreads();
   }
   const auto desc_of = [&](uint32_t t) {
@@ -1826,6 +1828,8 @@ void checksum_kernel_split(const KernelArgs args) {
   if (args.tail_scatter) {
     if constexpr (kShared) {
       if (shared_on) {
+        if (kPatchLastSlot && lane == 0 && it > 0)
+          __hip_atomic_store(&pq_last[wv], static_cast<uint32_t>(it - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint64_t tw0 = wall_clock64();
         for (;;) {
           uint32_t h = 0;
@@ -1840,9 +1844,15 @@ void checksum_kernel_split(const KernelArgs args) {
             __builtin_amdgcn_s_sleep(2);
           }
           if (m == 0) break;
-          if (m != kPQNull)
-            tail_patch_list(args, lds_addr(&plist[(m - 1) >> 8][0]) + 8 * ((m - 1) & 0xffu) * kWave, 1, lane, false,
-                            area, kSlot);
+          if (m != kPQNull) {
+            const uint32_t w2 = (m - 1) >> 8, t2 = (m - 1) & 0xffu;
+            // kPatchLastSlot: the unit is its wave's last, so that wave's slots still hold its windows
+            const bool in_slots = kPatchLastSlot &&
+                t2 == static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
+                          __hip_atomic_load(&pq_last[w2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))));
+            tail_patch_list(args, lds_addr(&plist[w2][0]) + 8 * t2 * kWave, 1, lane, in_slots,
+                            lds_addr(&slots[w2][0]), kSlot);
+          }
         }
       }
     }
