@@ -187,6 +187,7 @@ class HostPath:
         self.cs = checksummer
         self.umem = umem
         self.max_batch = int(max_batch)
+        self._pending = []   # (ticket, descs, verdicts) submitted and not yet waited for
         self._lib = _lib.load()
         self._ctx = ctypes.c_void_p()
         _lib.check(self._lib.xsknf_gpu_ctx_create(ctypes.byref(self._ctx), device, self.PATHS[path],
@@ -222,20 +223,20 @@ class HostPath:
         if descs.dtype.itemsize != 16 or not descs.flags.c_contiguous:
             raise ValueError("descs must be a contiguous array of 16-byte xdp_desc")
         n = int(descs.shape[0])
-        if verdicts.shape[0] < n or not verdicts.flags.c_contiguous:
+        if verdicts.dtype.itemsize != 4 or verdicts.dtype.kind != "i" or verdicts.shape[0] < n \
+                or not verdicts.flags.c_contiguous:
             raise ValueError("verdicts must be a contiguous int32 array with >= n entries")
         opts = self.cs.csum_opts()
         t = ctypes.c_uint64()
         _lib.check(self._lib.xsknf_gpu_ctx_submit(self._ctx, descs.ctypes.data, n, ingress_ifindex,
                                                   ctypes.byref(opts), verdicts.ctypes.data, ctypes.byref(t)),
                    "xsknf_gpu_ctx_submit")
-        self._pending = getattr(self, "_pending", [])
         self._pending.append((t.value, descs, verdicts))   # keep the arrays alive until waited for
         return t.value
 
     def wait(self, ticket: int) -> None:
         _lib.check(self._lib.xsknf_gpu_ctx_wait(self._ctx, ticket), "xsknf_gpu_ctx_wait")
-        self._pending = [p for p in getattr(self, "_pending", []) if p[0] > ticket]
+        self._pending = [p for p in self._pending if p[0] > ticket]
 
     def stats(self) -> dict:
         st = _lib.CtxStats()
