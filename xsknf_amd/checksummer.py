@@ -208,6 +208,8 @@ class HostPath:
         n = int(descs.shape[0])
         if verdicts is None:
             verdicts = np.empty(n, dtype=np.int32)
+        elif verdicts.dtype != np.int32 or verdicts.shape[0] < n or not verdicts.flags.c_contiguous:
+            raise ValueError("verdicts must be a contiguous int32 array with >= n entries")
         opts = self.cs.csum_opts()
         _lib.check(self._lib.xsknf_gpu_ctx_process_batch(self._ctx, descs.ctypes.data, n,
                                                          ingress_ifindex, ctypes.byref(opts),
