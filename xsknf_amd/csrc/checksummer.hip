@@ -1437,6 +1437,14 @@ void checksum_kernel_split(const KernelArgs args) {
   const uint32_t iq = kCompact ? area + 20 * kWave : lds_addr(&itemq[wv][0]);
   const uint32_t waves = gridDim.x * SW;
   const uint32_t last = args.n - 1;
+// Streaming waves issue ahead of patching ones: priority 1 until the wave's
+// last unit, 0 for its patches (with the patch queue below: 1500 B -0.9..-1.5
+// us, its NIC traffic -3 us, other sizes level -- profiles/r04/ab/ab_patch_prio_*;
+// XSKNF_PATCH_PRIO=0 for the A/B)
+#ifndef XSKNF_PATCH_PRIO
+#define XSKNF_PATCH_PRIO 1
+#endif
+  if (XSKNF_PATCH_PRIO) __builtin_amdgcn_s_setprio(1);
 
   uint32_t nrec = 0;
 #ifdef XSKNF_TIMELINE
@@ -1513,17 +1521,19 @@ void checksum_kernel_split(const KernelArgs args) {
     tnn = t0 + 2 * waves < ntiles ? t0 + 2 * waves : kNoTile;
   }
 #ifndef XSKNF_PATCH_SHARED
-#define XSKNF_PATCH_SHARED 0
+#define XSKNF_PATCH_SHARED 1
 #endif
-  // (A/B) One patch queue per block instead of each wave patching its own list
+  // One patch queue per block (the pooled shapes) instead of each wave patching its own list
   // after its last unit: a wave publishes each finished unit's list (its index,
   // or a null mark for a unit with nothing to patch), and a wave whose stream
   // is done takes the next published unit of ANY wave of the block, so the
   // block's last stream is followed by one unit's patches, not by its wave's
   // whole list.  Every wave publishes one mark per unit; the block's count of
   // units is known, so the consumers' loop ends; the wait for a mark is bounded
-  // by the clock.  Measured: 1500 B -0.8..-1.5 us, the launch still ends ~7 us
-  // after its last stream (profiles/r04/ab/ab_patch_queue_*): not the product.
+  // by the clock.  Measured alone: 1500 B -0.8..-1.5 us, the launch still ends
+  // ~7 us after its last stream (profiles/r04/ab/ab_patch_queue_*); with the
+  // streaming waves' priority (XSKNF_PATCH_PRIO) the product's since round 4.
+  // XSKNF_PATCH_SHARED=0: each wave patches its own list (A/B).
   constexpr bool kShared = XSKNF_PATCH_SHARED && PT > 0 && kPool;   // (static 4-wave IMIX: +1 us)
   constexpr uint32_t kPQ = kShared ? SW * PT : 1;   // marks: the grid is sized so a block has <= SW * PT units
   constexpr uint32_t kPQNull = 0xffffu;
@@ -1826,6 +1836,7 @@ void checksum_kernel_split(const KernelArgs args) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long tl1 = wall_clock64();
 #endif
+  if (XSKNF_PATCH_PRIO) __builtin_amdgcn_s_setprio(0);
   if (args.tail_scatter) {
     if constexpr (kShared) {
       if (shared_on) {
