@@ -376,10 +376,12 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     lib = _lib.load()
     cfg = cs.launch_cfg()
     # one launch per step: every check in-line (mode 1), or deferred and patched
-    # by each wave after its last tile (+16, split kernel)
+    # in the same launch once the waves' streams are done (+16, split kernel)
     single_kernel = (cfg.fused_stores & 3) == 1 or bool(cfg.fused_stores & 16)
     stores = ("checks in-line" if (cfg.fused_stores & 3) == 1 else
-              "checks deferred, each wave patches its own tiles" if cfg.fused_stores & 16 else
+              ("checks deferred, patched from the block's queue by waves done streaming"
+               if cfg.kernel == 1 and cfg.window_chunks & 32 else
+               "checks deferred, each wave patches its own tiles") if cfg.fused_stores & 16 else
               "checks deferred to a scatter_checks launch")
     family = ("checksum_kernel_split" if cfg.kernel == 1 else
               "checksum_kernel_lane" if cfg.lanes_per_frame == 1 else "checksum_kernel")

@@ -115,8 +115,8 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * that whole sector (group and lane kernels); adding 4 to `fused_stores` writes
  * the 2 check bytes alone instead, adding 8 makes the lane kernel's sector
  * stores plain (write-back) rather than non-temporal (A/B).  Adding 16 (split
- * kernel) patches the deferred checks in the summing kernel itself, each wave
- * its own tiles after its last one, instead of a second launch (the default
+ * kernel) patches the deferred checks in the summing kernel itself, once the
+ * waves' streams are done, instead of a second launch (the default
  * with 2 up to 4 KiB frames: every check deferred, then patched in bursts at
  * the waves' ends).
  * A frame whose computed check equals the check it already holds (traffic whose

@@ -37,9 +37,10 @@
 // * Stores (default_cfg): frames <= 128 B write each check in-line as its
 //   whole 64-byte sector.  Up to 4 KiB every check is deferred -- writes mixed
 //   into the read stream cost several times their bytes (tools/hbm_probe) --
-//   into the wave's LDS patch list (sector index + check); after its last tile
-//   the wave rewrites each listed sector whole (tail_patch_list), with no
-//   second launch.  Jumbo tiles park check records in `verdicts` for a
+//   into the wave's LDS patch list (sector index + check); once the stream is
+//   done each listed sector is rewritten whole (tail_patch_list), with no second
+//   launch: by the wave itself after its last tile (4-wave blocks), or by any
+//   wave of the block done streaming, from the block's queue (pooled blocks).  Jumbo tiles park check records in `verdicts` for a
 //   write-only scatter_checks pass (per-tile policy).
 #include <hip/hip_runtime.h>
 #include <atomic>
@@ -2794,8 +2795,8 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   //    [split kernel 60.3-61.3];
   //  * <= 4 KiB: the split kernel, 8-chunk window (the frame's whole first
   //    128-byte line, so phase B never refetches it), 16 x 2 items, two in
-  //    flight, every check deferred and patched by each wave after its last
-  //    tile, two tiles' patches in flight (no second launch): 570 B 148.8 us
+  //    flight, every check deferred and patched once the stream is done
+  //    (no second launch; round 4: the pooled blocks from one queue): 570 B 148.8 us
   //    [in-line 170.2], IMIX 117.8 [per-tile policy + scatter pass 125-136,
   //    all in-line 127], 1500 B 291.6-292.5 [16 x 3 items + scatter pass
   //    294.4-297.4]; one 12-wave block per CU whose waves share the CU's
