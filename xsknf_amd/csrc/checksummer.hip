@@ -1535,7 +1535,10 @@ void checksum_kernel_split(const KernelArgs args) {
   // ~7 us after its last stream (profiles/r04/ab/ab_patch_queue_*); with the
   // streaming waves' priority (XSKNF_PATCH_PRIO) the product's since round 4.
   // XSKNF_PATCH_SHARED=0: each wave patches its own list (A/B).
-  constexpr bool kShared = XSKNF_PATCH_SHARED && PT > 0 && kPool;   // (static 4-wave IMIX: +1 us)
+#ifndef XSKNF_PATCH_SHARED_STATIC   // (A/B) the queue in the static 4-wave blocks too (alone: IMIX +1 us)
+#define XSKNF_PATCH_SHARED_STATIC 0
+#endif
+  constexpr bool kShared = XSKNF_PATCH_SHARED && PT > 0 && (kPool || XSKNF_PATCH_SHARED_STATIC);
   constexpr uint32_t kPQ = kShared ? SW * PT : 1;   // marks: the grid is sized so a block has <= SW * PT units
   constexpr uint32_t kPQNull = 0xffffu;
   __shared__ uint32_t pq_tail, pq_head;
