@@ -555,12 +555,34 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(res, budget_s, threads, check=True):
+def _cpu_list(cpus) -> str:
+    """A CPU set as ranges ("0-15,32")."""
+    out, run = [], []
+    for c in sorted(cpus):
+        if run and c == run[-1] + 1:
+            run.append(c)
+            continue
+        if run:
+            out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+        run = [c]
+    if run:
+        out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+    return ",".join(out)
+
+
+def cpu_baseline(res, budget_s, threads, check=True, windows=3):
     """The reference's own xsknf_packet_processor() (oracle/_ref: its verbatim
     text compiled gcc -O2 -flto, kind "reference") -- or, where that library was
     not built, the C restatement (kind "port") -- timed on host cores in a
     process_batch_1if-shaped loop over a bounded sample of the same workload;
-    also checks the GPU result on that sample."""
+    also checks the GPU result on that sample.
+
+    `windows` timed windows of budget_s / windows each; `value` is their
+    median, `spread` their min / max.  One thread is pinned to the LAST CPU of
+    the process's affinity mask (the reference's tests pin the NF to one core,
+    tests/test-drop-cpu.py:79; the first CPU of the mask is where the HIP
+    runtime's threads of this process tend to run); several threads take the
+    mask's last `threads` CPUs."""
     from oracle import csum_oracle as O
     from oracle import ref as R
 
@@ -570,10 +592,14 @@ def cpu_baseline(res, budget_s, threads, check=True):
     umem_host, descs_host, k = res["sample"]
     lens = descs_host["len"].astype(np.int64)
     work = umem_host.copy()
-    t1, v = timer(work, descs_host, threads=threads, reps=1)
-    reps = max(1, int(budget_s / max(t1, 1e-6)))
-    t, v = timer(work, descs_host, threads=threads, reps=reps)
-    gbs = lens.sum() * reps / t / 1e9
+    t1, v = timer(work, descs_host, threads=threads, reps=1, pin="last")
+    reps = max(1, int(budget_s / windows / max(t1, 1e-6)))
+    rates, secs = [], 0.0
+    for _ in range(max(1, windows)):
+        t, v = timer(work, descs_host, threads=threads, reps=reps, pin="last")
+        rates.append(lens.sum() * reps / t / 1e9)
+        secs += t
+    gbs = float(np.median(rates))
     # checker: GPU output on the sample frames == the CPU path's output (single
     # pass; reprocessing is idempotent because the check is cleared before summing)
     match = None
@@ -583,12 +609,19 @@ def cpu_baseline(res, budget_s, threads, check=True):
         g_umem = res["umem"][:hi].cpu().numpy()
         g_v = res["verdicts"][:k].cpu().numpy()
         match = bool(np.array_equal(g_v, v) and np.array_equal(g_umem, umem_host))
-    return {"value": round(float(gbs), 4), "unit": "GB/s checksummed", "cores": threads,
+    mask = sorted(os.sched_getaffinity(0))
+    used = mask[-threads:] if threads <= len(mask) else mask
+    frames_per_gb = k / lens.sum()
+    return {"value": round(gbs, 4), "unit": "GB/s checksummed", "cores": threads,
+            "spread": {"min": round(float(min(rates)), 4), "max": round(float(max(rates)), 4),
+                       "windows": len(rates), "statistic": "median of the windows"},
             "kind": kind, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-            "mpps": round(k * reps / t / 1e6, 4),
-            "sample": f"{k} frames of the same workload ({lens.sum() / 1e6:.1f} MB) x {reps} passes, "
-                      f"{t:.1f} s, process_batch_1if-shaped loop (batch 64), 1 pinned core"
-                      if threads == 1 else f"{k} frames x {reps} passes, {threads} threads",
+            "affinity_mask": _cpu_list(mask), "pinned_to": _cpu_list(used),
+            "mpps": round(gbs * frames_per_gb * 1e3, 4),
+            "sample": f"{k} frames of the same workload ({lens.sum() / 1e6:.1f} MB) x {reps} passes per window, "
+                      f"{len(rates)} windows, {secs:.1f} s, process_batch_1if-shaped loop (batch 64), "
+                      + ("1 core pinned to the last CPU of the mask" if threads == 1 else
+                         f"{threads} threads on {threads} of the box's {len(mask)}-CPU share"),
             "gpu_matches_oracle_on_sample": match,
             "code": "oracle/_ref/libcsum_ref.so: reference checksummer_user.c:30-112 verbatim, gcc -O2 -flto"
                     if kind == "reference" else "oracle/csum_oracle.c (restatement), gcc -O2 -flto"}
@@ -767,7 +800,8 @@ def main():
             n_all = min(16, len(os.sched_getaffinity(0)))
         if n_all > 1:
             allc = cpu_baseline(prim, args.cpu_seconds / 2, n_all, check=False)
-            cpu["all_cores"] = {k: allc[k] for k in ("value", "unit", "cores", "mpps", "sample")}
+            cpu["all_cores"] = {k: allc[k] for k in ("value", "unit", "cores", "mpps", "spread", "pinned_to",
+                                                     "sample")}
     if rank == 0:
         length, layout, chunk, desc = WORKLOADS[args.workload]
         out = {

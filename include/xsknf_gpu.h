@@ -114,11 +114,13 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * In-line checks whose 64-byte sector lies inside the frame are written as
  * that whole sector (group and lane kernels); adding 4 to `fused_stores` writes
  * the 2 check bytes alone instead, adding 8 makes the lane kernel's sector
- * stores plain (write-back) rather than non-temporal (A/B).  Adding 16 (split
- * kernel) patches the deferred checks in the summing kernel itself, once the
- * waves' streams are done, instead of a second launch (the default
- * with 2 up to 4 KiB frames: every check deferred, then patched in bursts at
- * the waves' ends).
+ * stores plain (write-back) rather than non-temporal (A/B); where the 64 frames
+ * of a lane-kernel step lie apart (a 2 KiB-chunk UMEM) its sector stores are
+ * written through the L2 (sc1 nt).  Adding 16 (split kernel) patches the
+ * deferred checks in the summing kernel itself, once the waves' streams are
+ * done, instead of a second launch (the default with 2 for every frame length
+ * past the lane kernel's: every check deferred, then patched in bursts at the
+ * waves' ends; jumbo frames too since round 5).
  * A frame whose computed check equals the check it already holds (traffic whose
  * UDP checksums a NIC filled in, tests/gen-traffic.lua:120) ends with the bytes
  * it began with (:68 clears the check, :108 stores the same value), so the
@@ -134,7 +136,8 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * `window_chunks` + 16 loads the windows transposed (W lanes per frame, one
  * coalesced request); + 32 (with + 16, W = 8, 16 x 2 items, two in flight)
  * launches one 12-wave block per CU whose waves draw the CU's tiles from a
- * shared pool (the default up to 4 KiB frames).  Only instantiated shapes are accepted (-EINVAL
+ * shared pool (the default up to 4 KiB frames; W = 4, 16 x 3: one 8-wave block
+ * per CU, the jumbo default).  Only instantiated shapes are accepted (-EINVAL
  * otherwise); every shape gives identical results.
  */
 #define XSKNF_GPU_RECORD_TAG 0x40000000u       /* bits 31..30 = 01 */

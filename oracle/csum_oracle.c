@@ -168,7 +168,7 @@ static void *worker(void *p)
 /*
  * Run `reps` passes of the batch loop over `n` frames, split contiguously
  * over `threads` pthreads (each pinned to the i-th CPU of the affinity mask
- * when pin != 0).  Returns wall seconds (CLOCK_MONOTONIC), or -1 on error.
+ * when pin == 1, the i-th from its end when pin == 2).  Returns wall seconds (CLOCK_MONOTONIC), or -1 on error.
  */
 double oracle_time_batch(uint8_t *umem, const struct oracle_desc *descs,
 		uint32_t n, const struct oracle_opts *o, int32_t *verdicts,
@@ -182,9 +182,18 @@ double oracle_time_batch(uint8_t *umem, const struct oracle_desc *descs,
 	cpu_set_t mask;
 	int ncpu = 0;
 	if (pin && sched_getaffinity(0, sizeof(mask), &mask) == 0) {
-		for (int c = 0; c < CPU_SETSIZE && ncpu < threads; c++)
-			if (CPU_ISSET(c, &mask))
-				cpus[ncpu++] = c;
+		/* pin 1: the first CPUs of the mask; pin 2: the last ones (away
+		 * from CPU 0 of the mask, where the HIP runtime's threads of the
+		 * calling process tend to run) */
+		if (pin == 2) {
+			for (int c = CPU_SETSIZE - 1; c >= 0 && ncpu < threads; c--)
+				if (CPU_ISSET(c, &mask))
+					cpus[ncpu++] = c;
+		} else {
+			for (int c = 0; c < CPU_SETSIZE && ncpu < threads; c++)
+				if (CPU_ISSET(c, &mask))
+					cpus[ncpu++] = c;
+		}
 	}
 	struct timespec t0, t1;
 	clock_gettime(CLOCK_MONOTONIC, &t0);

@@ -78,12 +78,20 @@ def c_process_batch(umem: np.ndarray, descs: np.ndarray, ingress=0, iters=1, act
     return v
 
 
+def _pin_mode(pin) -> int:
+    """pin: False (unpinned), True / "first" (the first CPUs of the affinity
+    mask), "last" (the last ones, away from the HIP runtime's threads)."""
+    if pin == "last":
+        return 2
+    return 1 if pin else 0
+
+
 def c_time_batch(umem, descs, iters=1, action=REDIRECT, nif=1, threads=1, reps=1, pin=True):
     n = int(descs.shape[0])
     v = np.empty(n, dtype=np.int32)
     t = load().oracle_time_batch(umem.ctypes.data, descs.ctypes.data, n,
                                  ctypes.byref(_opts(iters, action, nif)), v.ctypes.data,
-                                 threads, reps, 1 if pin else 0)
+                                 threads, reps, _pin_mode(pin))
     if t < 0:
         raise RuntimeError("oracle_time_batch failed")
     return t, v

@@ -76,13 +76,21 @@ def process_batch(umem: np.ndarray, descs: np.ndarray, ingress=0, iters=1, actio
     return v
 
 
+def _pin_mode(pin) -> int:
+    """pin: False (unpinned), True / "first" (the first CPUs of the affinity
+    mask), "last" (the last ones, away from the HIP runtime's threads)."""
+    if pin == "last":
+        return 2
+    return 1 if pin else 0
+
+
 def time_batch(umem, descs, iters=1, action=REDIRECT, nif=1, threads=1, reps=1, pin=True):
     lib = load()
     lib.ref_set_options(int(iters), int(action), int(nif))
     n = int(descs.shape[0])
     v = np.empty(n, dtype=np.int32)
     t = lib.ref_time_batch(umem.ctypes.data, descs.ctypes.data, n, v.ctypes.data, threads, reps,
-                           1 if pin else 0)
+                           _pin_mode(pin))
     if t < 0:
         raise RuntimeError("ref_time_batch failed")
     return t, v

@@ -87,7 +87,8 @@ static void *ref_worker_main(void *p)
 }
 
 /* `reps` passes over n frames split contiguously over `threads` pthreads
- * (pinned to the first CPUs of the affinity mask when pin != 0); the options
+ * (pinned to the first CPUs of the affinity mask when pin == 1, the last
+ * ones when pin == 2); the options
  * are whatever ref_set_options() last set.  Wall seconds, or -1. */
 double ref_time_batch(uint8_t *umem, const struct ref_desc *descs, uint32_t n,
 		int32_t *verdicts, int threads, int reps, int pin)
@@ -100,9 +101,18 @@ double ref_time_batch(uint8_t *umem, const struct ref_desc *descs, uint32_t n,
 	cpu_set_t mask;
 	int ncpu = 0;
 	if (pin && sched_getaffinity(0, sizeof(mask), &mask) == 0) {
-		for (int c = 0; c < CPU_SETSIZE && ncpu < threads; c++)
-			if (CPU_ISSET(c, &mask))
-				cpus[ncpu++] = c;
+		/* pin 1: the first CPUs of the mask; pin 2: the last ones (away
+		 * from CPU 0 of the mask, where the HIP runtime's threads of the
+		 * calling process tend to run) */
+		if (pin == 2) {
+			for (int c = CPU_SETSIZE - 1; c >= 0 && ncpu < threads; c--)
+				if (CPU_ISSET(c, &mask))
+					cpus[ncpu++] = c;
+		} else {
+			for (int c = 0; c < CPU_SETSIZE && ncpu < threads; c++)
+				if (CPU_ISSET(c, &mask))
+					cpus[ncpu++] = c;
+		}
 	}
 	struct timespec t0, t1;
 	clock_gettime(CLOCK_MONOTONIC, &t0);

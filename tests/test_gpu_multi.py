@@ -7,8 +7,9 @@
   pass over the whole batch;
 * the root distribution (scatter_from_root) with two ranks on gloo, both on
   cuda:0, the HIP kernel run on the shards each rank received;
-* `bench.py --gpus 2` started by hand on a one-GPU box starts its two ranks
-  itself (gloo rehearsal) and reports n_gpus = 2.
+* `bench.py --gpus N` (N = 2, 4) started by hand on a one-GPU box starts its
+  N ranks itself (gloo rehearsal), reports n_gpus = N, splits config 4 N ways
+  and delivers every frame of the root distribution.
 
 Processes are started from the forkserver of tests/conftest.py, never from this
 (GPU-initialised) process.
@@ -139,32 +140,41 @@ def _run(cmd, env, timeout):
     return p.returncode, p.stdout, p.stderr
 
 
-def test_bench_gpus_n_starts_its_ranks(dev, clean_ctx):
-    """`python bench.py --gpus 2` (no torch.distributed.run around it) starts two
-    ranks itself; on a one-GPU box they rehearse over gloo; rank 0 reports
-    n_gpus = 2 and both ranks' frames, and config 4's global batch is split
-    between them."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_gpus_n_starts_its_ranks(dev, clean_ctx, world):
+    """`python bench.py --gpus N` (no torch.distributed.run around it) starts N
+    ranks itself (the reference's one worker per queue, src/xsknf.c:1046-1100);
+    on a one-GPU box they rehearse over gloo; rank 0 reports n_gpus = N and
+    every rank's frames, config 4's global batch is split N ways by bytes (rank
+    0 holds exactly shard_by_bytes' first range), and the root distribution
+    delivers every frame and matches the single-GPU pass."""
+    from xsknf_amd import frames as F
+    from xsknf_amd.shard import shard_by_bytes
     env = dict(os.environ)
-    if torch.cuda.device_count() < 2:
+    if torch.cuda.device_count() < world:
         env["XSKNF_BENCH_BACKEND"] = "gloo"
-    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--frames", "65536",
-           "--secondary", "config4", "--config4-frames", "131072", "--cpu-seconds", "0", "--kernel-steps", "0",
+    c4 = 131072
+    cmd = [sys.executable, "bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "1", "--frames", "65536",
+           "--secondary", "config4", "--config4-frames", str(c4), "--cpu-seconds", "0", "--kernel-steps", "0",
            "--min-warmup-s", "0"]
     with clean_ctx.Pool(1) as pool:
         rc, out, err = pool.apply(_run, (cmd, env, 400))
     assert rc == 0, err[-3000:]
     line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2
-    assert line["config"]["global_batch"] == 2 * 65536
-    assert line["verdicts"]["forward"] == 2 * 65536
-    assert line["secondary"]["config4"]["frames"] == 131072
+    assert line["n_gpus"] == world
+    assert line["config"]["global_batch"] == world * 65536
+    assert line["verdicts"]["forward"] == world * 65536
+    assert line["secondary"]["config4"]["frames"] == c4
+    glens = F.imix_lengths(c4, np.random.default_rng(F.SEED))
+    assert line["secondary"]["config4"]["rank0_shard"] == list(shard_by_bytes(glens, world)[0])
     assert line["roofline"]["frac"] > 0
-    # self-checking multi-rank line: the backend saw both ranks, and the root
+    # self-checking multi-rank line: the backend saw every rank, and the root
     # distribution ran by default and delivered every frame
-    assert line["dist"]["ranks_seen"] == 2 and line["dist"]["world_size"] == 2
-    assert line["dist"]["frames_allreduced"] == 2 * 65536
-    assert line["root_scatter"]["frames_total"] == 2 * 65536
+    assert line["dist"]["ranks_seen"] == world and line["dist"]["world_size"] == world
+    assert line["dist"]["frames_allreduced"] == world * 65536
+    assert line["root_scatter"]["frames_total"] == world * 65536
     assert line["root_scatter"]["vs_single_gpu"]["match"] is True
+    assert line["root_scatter"]["rfc_check"]["violations"] == 0
 
 
 def test_rccl_collectives_on_one_gpu(dev, clean_ctx):

@@ -924,7 +924,7 @@ TL_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 @pytest.mark.skipif(not os.path.exists(TL_LIB), reason="timeline build absent (make tl)")
 @pytest.mark.parametrize("frames_n,bpc", [(600_000, 1), (1 << 20, 1), (1 << 20, 8)])
-@pytest.mark.parametrize("window,limit", [(24, 6), (56, 7)], ids=["static", "pool"])
+@pytest.mark.parametrize("window,limit", [(24, 6), (56, 7), (52, 16)], ids=["static", "pool", "pool-jumbo"])
 def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
     """launch_split sizes the grid so that no wave of a patch-list shape gets
     more tiles than its list holds (static: each wave's share of the tiles;
@@ -937,7 +937,7 @@ def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
     env = dict(os.environ, XSKNF_GPU_LIB=TL_LIB)
     out = subprocess.run([sys.executable, os.path.join(root, "tools", "timeline.py"), "--workload", "imix",
                           "--frames", str(frames_n), "--reps", "2", "--bpc", str(bpc),
-                          "--variant", f"16,2,2,0,18,1,{window}"],
+                          "--variant", f"16,{3 if window == 52 else 2},2,0,18,1,{window}"],
                          capture_output=True, text=True, timeout=240, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
     med = json.loads(out.stdout.strip().splitlines()[-1])["median"]
@@ -946,10 +946,12 @@ def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
     assert max(tiles) <= limit, tiles
 
 
-@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 0, 1, 52),
+@pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 18, 1, 52), (16, 3, 2, 0, 0, 1, 52),
                                    pytest.param((1, 5, 2, 0, 1, 0, 32),
+                                                marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only")),
+                                   pytest.param((1, 5, 1, 0, 1, 0, 32),
                                                 marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only"))],
-                         ids=["pool-w8", "pool-jumbo", "pool-lane"])
+                         ids=["pool-w8", "pool-jumbo", "pool-jumbo-scatter", "pool-lane", "pool-lane-64"])
 @pytest.mark.parametrize("n", [1, 17, 33, 95, 12 * 64 + 5, 3 * 12 * 64 - 7, 256 * 12 * 64 + 4095])
 def test_pool_units_cover_every_frame(dev, shape, n):
     """The CU-wide tile pool (window + 32): the block's last tiles run as

@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 
 from xsknf_amd import _lib, frames  # noqa: E402
 
-WL = {"1500": (1500, "aligned"), "imix": ("imix", "aligned"), "570": (570, "aligned"),
+WL = {"1500": (1500, "aligned"), "imix": ("imix", "aligned"), "570": (570, "aligned"), "64": (64, "aligned"),
       "1024": (1024, "aligned"), "jumbo": (9000, "unaligned")}
 
 
@@ -100,7 +100,10 @@ def main():
         gw = np.nonzero(t[:, 0] != 0)[0]
         t = t[t[:, 0] != 0]
         cus = torch.cuda.get_device_properties(0).multi_processor_count
-        wpb = 12 if cfg.window_chunks & 32 else 4   # waves per block (window + 32: one 12-wave block per CU)
+        # waves per block (window + 32: one block per CU, 12 waves; 8 for jumbo's W = 4)
+        wpb = 4
+        if cfg.window_chunks & 32:   # one block per CU: split 12 waves (8 for jumbo's W = 4), lane 16
+            wpb = (12 if (cfg.window_chunks & 15) == 8 else 8) if cfg.kernel == 1 else 16
         bslot, xcd, wvi = (gw // wpb) // cus, (gw // wpb) % 8, gw % 4
         blk = gw // wpb
         sd_us = (t[:, 1] - t[:, 0].min()) / 100.0

@@ -35,13 +35,15 @@
 // * Group partial sums reduce with DPP (row_shr / row_bcast) into the group's
 //   last lane.
 // * Stores (default_cfg): frames <= 128 B write each check in-line as its
-//   whole 64-byte sector.  Up to 4 KiB every check is deferred -- writes mixed
-//   into the read stream cost several times their bytes (tools/hbm_probe) --
-//   into the wave's LDS patch list (sector index + check); once the stream is
-//   done each listed sector is rewritten whole (tail_patch_list), with no second
-//   launch: by the wave itself after its last tile (4-wave blocks), or by any
-//   wave of the block done streaming, from the block's queue (pooled blocks).  Jumbo tiles park check records in `verdicts` for a
-//   write-only scatter_checks pass (per-tile policy).
+//   whole 64-byte sector (written through L2 where the frames lie apart).
+//   Longer frames defer every check -- writes mixed into the read stream cost
+//   several times their bytes (tools/hbm_probe) -- into the wave's LDS patch
+//   list (sector index + check); once the stream is done each listed sector is
+//   rewritten whole (tail_patch_list), with no second launch: by the wave
+//   itself after its last tile (4-wave blocks), or by any wave of the block
+//   done streaming, from the block's queue (pooled blocks, jumbo included).
+//   Only the modes that ask for it (fused_stores 0) park check records in
+//   `verdicts` for a write-only scatter_checks pass.
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <mutex>
@@ -732,6 +734,27 @@ __device__ __forceinline__ void store_lane_tl(uint32_t area, const uint4 (&x)[NC
   }
 }
 
+#ifdef XSKNF_TIMELINE
+// A/B instrument (tools/timeline.py): per wave of the split and lane kernels, the
+// constant 100 MHz clock at its start, after its last tile, after its patches,
+// and its tile count, so the step can be split into stream and patch time.
+__device__ unsigned long long *g_timeline;
+// 8 u64 per wave: start, stream done, patches done, tiles, then the clock
+// summed over the wave's tiles in phase A (window loads until they are in
+// LDS), phase A's parse, and phase B (payload items)
+__device__ __forceinline__ void timeline_put(uint32_t wave, int lane, unsigned long long t0, unsigned long long t1,
+                                             int tiles, unsigned long long sa, unsigned long long sp,
+                                             unsigned long long sb) {
+  const unsigned long long t2 = wall_clock64();
+  unsigned long long *p = g_timeline;
+  const unsigned long long v[8] = {t0, t1, t2, static_cast<unsigned long long>(tiles), sa, sp, sb, 0ull};
+  unsigned long long x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x = lane == k ? v[k] : x;
+  if (p && lane < 8) p[8ull * wave + lane] = x;
+}
+#endif
+
 // A lane's result; when `sector` is set, the frame's patched 64-byte check
 // sector sits in the lane's LDS slot at `lds_sec`, to be written to `gsec` by
 // the wave's cooperative store (store_sectors).
@@ -795,10 +818,32 @@ __device__ __forceinline__ LaneOut process_lane(const KernelArgs &args, const Fr
   return out;
 }
 
+#ifndef XSKNF_LANE_WT   // 0 (A/B): every in-line sector non-temporal
+#define XSKNF_LANE_WT 1
+#endif
+// One 16-byte piece of an in-line check sector: non-temporal, or (wt) sc1 nt,
+// written through the XCD's L2 at once.  Frames 2 KiB apart (the aligned
+// UMEM) share no line, and there the write-through store leaves no dirty line
+// for the end of the launch to write back: 64 B 58.0-58.3 vs 60.1-60.5 us; for
+// frames packed back to back (-u) it costs 38.2 -> 42.2 us, sectors there
+// sharing their 128-byte lines (profiles/r05/ab/ab_lane_sc*.jsonl; sc1 alone
+// and sc0 sc1: no gain).
+__device__ __forceinline__ void store_sector16(uint8_t *p, uint4 v, bool wt XSKNF_SITE) {
+  if (!wt) {
+    store_nt16(p, v);
+    return;
+  }
+#ifdef XSKNF_GUARD
+  if (!guard_ok(p, 16, site)) return;
+#endif
+  const u32x4 x = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(x) : "memory");
+}
+
 // The wave's patched sectors, 16 per instruction: lanes 4i..4i+3 write the 4
 // pieces of lane (16p + i)'s sector -- one coalesced 64-byte request each,
 // instead of 4 separate 16-byte stores per lane.
-__device__ __forceinline__ void store_sectors(const LaneOut &o, int lane, bool plain) {
+__device__ __forceinline__ void store_sectors(const LaneOut &o, int lane, bool plain, bool wt = false) {
   const uint64_t any = __builtin_amdgcn_ballot_w64(o.sector);
   if (!any) return;
   compiler_barrier();
@@ -818,7 +863,7 @@ __device__ __forceinline__ void store_sectors(const LaneOut &o, int lane, bool p
       if (plain) {
         XSKNF_GST(g + 16 * (lane & 3), 16) *reinterpret_cast<uint4 *>(g + 16 * (lane & 3)) = w;
       } else {
-        store_nt16(g + 16 * (lane & 3), w);
+        store_sector16(g + 16 * (lane & 3), w, wt);
       }
     }
   }
@@ -868,11 +913,18 @@ void checksum_kernel_lane(const KernelArgs args) {
     return *XSKNF_GLD(reinterpret_cast<const uint4 *>(args.descs + (t == kNoTile ? last : min(t * T + st * kWave + lane, last))), 16);
   };
   uint32_t nrec = 0;
+#ifdef XSKNF_TIMELINE
+  const unsigned long long tl0 = wall_clock64();
+  int tl_tiles = 0;
+#endif
   uint4 dn[SPT];
 #pragma unroll
   for (int st = 0; st < SPT; ++st) dn[st] = desc_at(tile, st);
   while (tile != kNoTile) {
     const uint32_t tf0 = tile * T;
+#ifdef XSKNF_TIMELINE
+    ++tl_tiles;
+#endif
     uint32_t next;
     if constexpr (kPool) {
       uint32_t dq = 0;
@@ -892,7 +944,8 @@ void checksum_kernel_lane(const KernelArgs args) {
     FrameRef r[2];
     r[0] = lane_ref(args, d[0], tf0 + lane);
     bool tl = TLM == 1;
-    if constexpr (TLM == 2) {
+    bool wt = false;   // in-line sectors written through (store_sector16)
+    if constexpr (TLM == 2 || XSKNF_LANE_WT) {
       // the tile's first and last frames' offsets: 64 frames packed back to back
       // span a few KiB, 64 chunks of a 2 KiB-chunk UMEM 126 KiB
       const uint64_t off = reinterpret_cast<uintptr_t>(r[0].fp) - reinterpret_cast<uintptr_t>(args.umem);
@@ -900,7 +953,9 @@ void checksum_kernel_lane(const KernelArgs args) {
                           static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<int>(off >> 32), 0)) << 32;
       const uint64_t o1 = static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<int>(off), kWave - 1)) |
                           static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<int>(off >> 32), kWave - 1)) << 32;
-      tl = (o1 > o0 ? o1 - o0 : o0 - o1) >= static_cast<uint64_t>(kWave - 1) * 256;
+      const bool apart = (o1 > o0 ? o1 - o0 : o0 - o1) >= static_cast<uint64_t>(kWave - 1) * 256;
+      if constexpr (TLM == 2) tl = apart;
+      wt = XSKNF_LANE_WT && apart;
     }
     if (tl) load_lane_tl<NCH>(r[0], v[0]); else load_lane<NCH>(r[0], v[0]);
 #pragma unroll
@@ -926,13 +981,19 @@ void checksum_kernel_lane(const KernelArgs args) {
       } else {
         o = process_lane<NCH>(args, r[st & 1], v[st & 1], slot);
       }
-      store_sectors(o, lane, args.plain_sector);
+      store_sectors(o, lane, args.plain_sector, wt);
       const uint32_t f = tf0 + st * kWave + lane;
       nrec += store_result(args, f, f < args.n, o.res);
       compiler_barrier();   // the next frame rewrites this lane's header window
     }
     tile = next;
   }
+#ifdef XSKNF_TIMELINE
+  // stream done (last store issued), then its stores acknowledged
+  const unsigned long long tl1 = wall_clock64();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  timeline_put(blockIdx.x * SW + wv, lane, tl0, tl1, tl_tiles, 0, 0, 0);
+#endif
   publish_records(args, nrec, lane);
 }
 
@@ -1288,9 +1349,17 @@ constexpr bool compact_split() {
   return W == 8 && NCH == 2 && U == 1 && !DMA && !PFW && !kPool;
 }
 
+// The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
+// a 16-unit list (64 KiB of its block's 135 KiB): with every check deferred
+// (fused_stores 2 + 16) the block's queue patches them in the launch instead of
+// a scatter_checks pass (round 5: 9000 B 1448.4-1449.3 vs 1455.9-1457.9 us and
+// 1457.2-1458.1 vs 1461.6-1462.9 on a second box, NIC checks -4 us;
+// profiles/r05/ab/).
+constexpr int kJumboPatchUnits = 16;
 template <int W, int NCH, int U, bool DMA, bool PFW, bool kPool>
 constexpr int patch_list_tiles() {
   if constexpr (compact_split<W, NCH, U, DMA, PFW, kPool>()) return 4;
+  if constexpr (W == 4 && NCH == 3 && U >= 2 && kPool && !DMA && !PFW) return kJumboPatchUnits;
   return (W == 8 && U >= 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
 }
 
@@ -1371,26 +1440,6 @@ __device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t
   }
 }
 
-#ifdef XSKNF_TIMELINE
-// A/B instrument (tools/timeline.py): per wave of the split kernel, the
-// constant 100 MHz clock at its start, after its last tile, after its patches,
-// and its tile count, so the step can be split into stream and patch time.
-__device__ unsigned long long *g_timeline;
-// 8 u64 per wave: start, stream done, patches done, tiles, then the clock
-// summed over the wave's tiles in phase A (window loads until they are in
-// LDS), phase A's parse, and phase B (payload items)
-__device__ __forceinline__ void timeline_put(uint32_t wave, int lane, unsigned long long t0, unsigned long long t1,
-                                             int tiles, unsigned long long sa, unsigned long long sp,
-                                             unsigned long long sb) {
-  const unsigned long long t2 = wall_clock64();
-  unsigned long long *p = g_timeline;
-  const unsigned long long v[8] = {t0, t1, t2, static_cast<unsigned long long>(tiles), sa, sp, sb, 0ull};
-  unsigned long long x = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) x = lane == k ? v[k] : x;
-  if (p && lane < 8) p[8ull * wave + lane] = x;
-}
-#endif
 
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
@@ -1422,8 +1471,8 @@ void checksum_kernel_split(const KernelArgs args) {
   __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kCompact ? 1 : kItemCap];
   __shared__ __attribute__((aligned(16))) uint4 meta[SW][kScratch];
   __shared__ __attribute__((aligned(16))) uint32_t accb[SW][kScratch];
-  // (jumbo keeps no list: with the pool and a 16-unit list, patching after the last unit tied the
-  // scatter pass, 1463 vs 1461 us -- profiles/r02/ab_jumbo_tail.jsonl)
+  // (jumbo's 16-unit list: each wave patching its own list after its last unit tied the scatter
+  // pass, 1463 vs 1461 us -- profiles/r02/ab_jumbo_tail.jsonl; from the block's queue it is ahead)
   constexpr int PT = patch_list_tiles<W, NCH, U, DMA, PFW, kPool>();
   __shared__ __attribute__((aligned(16))) uint2 plist[SW][PT > 0 ? PT * kWave : 1];
 
@@ -2723,6 +2772,9 @@ const Variant kVariants[] = {
     {16, 2, 1, 0, &launch_split<8, 16, 2, 1, true, false, false, 16>, XSKNF_GPU_KERNEL_SPLIT, 152},
 #endif
     XSKNF_LP(5, 2),   // lane kernel with the tile pool: 64 B 59.65 vs 59.51 us, a tie (r02 ab_pool_lane.jsonl)
+    // ... in 64-frame units (r05 ab_lane_pool / r05c): 64 B 58.8-59.1 vs 58.5-58.7 static (both write-through),
+    // packed 64 B 37.3 vs 38.0-38.3, packed NIC 20.1-20.4 vs 22.4-22.7
+    XSKNF_LP(5, 1),
     // transposed window loads (r04 ab_lane_transposed*.jsonl): aligned 64 B NIC -1 us, worst case +0.3,
     // packed (-u) frames +1 us; per tile by the frames' spread: worst case +2 us (4 waves per SIMD forced)
     XSKNF_LT(5, 2), XSKNF_LT(4, 2), XSKNF_LT(5, 1), XSKNF_LA(5, 2), XSKNF_LA(5, 1),
@@ -2809,7 +2861,9 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   //  * jumbo: 4-chunk window, 16 x 3 items, two per group in flight, the
   //    per-tile policy + scatter pass: 9000 B 1467 us [tail patches 1491];
   //    one 8-wave block per CU with the tile pool (+ 32): 1456 vs 1466 [12-wave
-  //    blocks 1520; tail patches 1598] (profiles/r02/ab_pool_jumbo.jsonl).
+  //    blocks 1520; tail patches 1598] (profiles/r02/ab_pool_jumbo.jsonl);
+  //    round 5: every check deferred and patched from the block's queue
+  //    (2 + 16, no scatter launch): 1448-1449 vs 1456-1458 (profiles/r05/ab/).
   c.kernel = XSKNF_GPU_KERNEL_SPLIT;
   c.lanes_per_frame = 16;
   if (hint <= 128) {
@@ -2821,7 +2875,7 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
     c.window_chunks = 8 + 16 + (mean != 0 && mean < kPoolMinMean ? 0 : 32);
     c.chunks_per_lane = 2; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   } else {
-    c.window_chunks = 4 + 16 + 32; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 0;
+    c.window_chunks = 4 + 16 + 32; c.chunks_per_lane = 3; c.frames_per_group = 2; c.fused_stores = 2 + 16;
   }
 }
 
