@@ -106,7 +106,7 @@ clean:
 	rm -rf $(LIBDIR) xsknf_amd/bin build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean tools ab tl guard guard-rec
+.PHONY: all oracle asm clean tools ab tl guard
 
 # Guard build: every UMEM access of the split kernel's paths range-checked and
 # recorded instead of faulting (tools/guard_run.py).  Not the product.
@@ -115,13 +115,3 @@ guard: $(GDLIB)
 $(GDLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h Makefile
 	@mkdir -p build/guard
 	$(HIPCC) $(HIPFLAGS) -DXSKNF_GUARD -shared -o $@ $(SRCS)
-
-# Guard build with the round-2 record path restored (XSKNF_RECORD_PATH: a
-# static-schedule wave's tiles past its patch list park records in `verdicts`
-# and the wave patches them after its list) -- the path that was in the two
-# faulting GPU suites; tools/guard_stress.py.  Debug only, not the product.
-GRLIB := build/guard_rec/libxsknf_gpu.so
-guard-rec: $(GRLIB)
-$(GRLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h Makefile
-	@mkdir -p build/guard_rec
-	$(HIPCC) $(HIPFLAGS) -DXSKNF_GUARD -DXSKNF_RECORD_PATH -shared -o $@ $(SRCS)

@@ -92,9 +92,10 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
  * takes tiles of `frames_per_group` consecutive frames per group (the next
  * frame's loads in flight while the current one is reduced); the persistent
  * grid has `blocks_per_cu`
- * 256-thread blocks per CU (0 = 8).  `lds_ring` > 0 selects the LDS-DMA
- * kernel, which streams each wave's frames through a ring of that many LDS
- * slots (frames_per_group is then ignored); 0 selects the register kernel.
+ * 256-thread blocks per CU (0 = 8).  `lds_ring` must be 0 (an LDS-DMA ring
+ * kernel, measured slower, was A/B material until round 5; any other value is
+ * -EINVAL); `kernel` = XSKNF_GPU_KERNEL_AUTO with lanes_per_frame > 1 selects
+ * the register kernel.
  * `lanes_per_frame` = 1 selects the lane kernel for small frames: each lane
  * owns a frame, loads its first `chunks_per_lane` (5..7) chunks itself, and a
  * wave step covers 64 frames (`frames_per_group` = steps per tile); longer
@@ -143,7 +144,7 @@ XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
 #define XSKNF_GPU_RECORD_TAG 0x40000000u       /* bits 31..30 = 01 */
 #define XSKNF_GPU_RECORD_TAG_MASK 0xC0000000u
 
-#define XSKNF_GPU_KERNEL_AUTO 0    /* group register / lane / LDS-DMA kernel by the fields above */
+#define XSKNF_GPU_KERNEL_AUTO 0    /* group register / lane kernel by the fields above */
 #define XSKNF_GPU_KERNEL_SPLIT 1   /* headers by lane, payload by lane groups */
 
 struct xsknf_gpu_launch_cfg {

@@ -275,8 +275,7 @@ PRODUCT_SHAPES = [
 # every other family / shape: only in the A/B build (`make ab`, XSKNF_GPU_LIB=build/ab/libxsknf_gpu.so)
 AB_SHAPES = [
     (8, 1, 2, 0, 0), (8, 1, 8, 0, 1), (16, 2, 4, 0, 2), (32, 3, 4, 0, 1),
-    (64, 9, 2, 0, 2), (64, 2, 8, 0, 0), (8, 1, 1, 3, 2), (16, 2, 1, 3, 1), (32, 3, 1, 2, 0), (32, 3, 1, 3, 1),
-    (64, 4, 1, 3, 0), (64, 2, 1, 4, 1),
+    (64, 9, 2, 0, 2), (64, 2, 8, 0, 0),
     (4, 2, 4, 0, 1), (4, 2, 2, 0, 0), (4, 2, 4, 0, 5),
     (1, 5, 4, 0, 0), (1, 6, 2, 0, 9), (1, 7, 2, 0, 5),
     (8, 1, 4, 0, 5), (16, 2, 4, 0, 4), (32, 3, 4, 0, 5),
@@ -286,11 +285,10 @@ AB_SHAPES = [
     (16, 2, 1, 0, 5, 1, 20), (16, 3, 1, 0, 1, 1, 20), (16, 2, 1, 0, 1, 1, 24), (32, 3, 1, 0, 2, 1, 24),
     # 16 x 3 items with the 8-tile patch list (long-frame batches, not in the product)
     (16, 3, 2, 0, 18, 1, 24), (16, 3, 2, 0, 2, 1, 24), (16, 3, 2, 0, 0, 1, 24), (16, 3, 2, 0, 1, 1, 24),
-    (16, 3, 2, 0, 0, 1, 116), (16, 3, 2, 0, 18, 1, 116),
-    # the lane kernel with one 16-wave block per CU sharing the CU's tiles (window field 32)
+    # the lane kernel with one 16-wave block per CU sharing the CU's tiles (window field 32), 128- and
+    # 64-frame units
     (1, 5, 2, 0, 1, 0, 32), (1, 5, 2, 0, 9, 0, 32), (1, 5, 2, 0, 2, 0, 32), (1, 5, 2, 0, 0, 0, 32),
-    # split kernel with LDS-DMA phase B (ring 1) / window prefetch (ring 2): every check deferred only
-    (16, 2, 2, 1, 18, 1, 24), (16, 4, 1, 1, 2, 1, 24), (16, 2, 2, 2, 18, 1, 24), (16, 3, 1, 2, 2, 1, 24),
+    (1, 5, 1, 0, 1, 0, 32), (1, 5, 1, 0, 2, 0, 32),
 ]
 AB_BUILD = "ab" in os.path.basename(os.path.dirname(os.environ.get("XSKNF_GPU_LIB", "")))
 SHAPES = PRODUCT_SHAPES + [pytest.param(s, marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only"))

@@ -7,8 +7,12 @@ product assembly (`make asm` -> build/asm/checksummer-gfx950.s), ignoring
 labels, comments and directives.  Use it to tell whether profiles recorded at
 REV still describe the product's kernels:
 
-    python3 tools/asm_same.py <rev>
+    python3 tools/asm_same.py <rev> [--diff]
+
+--diff prints the instruction diff of every kernel that is not identical
+(a renamed twin is matched by name with its template arguments removed).
 """
+import difflib
 import os
 import re
 import subprocess
@@ -42,9 +46,11 @@ def kernels(path):
 
 
 def main():
-    if len(sys.argv) != 2:
+    args = [a for a in sys.argv[1:] if a != "--diff"]
+    show = "--diff" in sys.argv[1:]
+    if len(args) != 1:
         raise SystemExit(__doc__)
-    rev = sys.argv[1]
+    rev = args[0]
     cur = os.path.join(ROOT, "build", "asm", "checksummer-gfx950.s")
     subprocess.run(["make", "-C", ROOT, "asm"], check=True, stdout=subprocess.DEVNULL)
     with tempfile.TemporaryDirectory() as d:
@@ -77,6 +83,17 @@ def main():
     for j in new:
         bad += 1
         print(f"only now: {j}")
+    if show:
+        # differing kernels, and kernels present on one side only paired by family name
+        fam = lambda k: re.sub(r"I.*E(EvNS|vNS)", "", k)
+        pairs = [(k, k) for k in sorted(set(a) & set(b)) if a[k] != b[k]]
+        pairs += [(k, j) for k in gone for j in new if fam(k) == fam(j) and
+                  len(set(a[k]) ^ set(b[j])) < 200]
+        for k, j in pairs:
+            print(f"--- {k} ({rev})\n+++ {j} (now)")
+            for line in difflib.unified_diff(a[k], b[j], lineterm="", n=0):
+                if not line.startswith(("---", "+++")):
+                    print(line)
     print(f"{same} kernels identical to {rev}, {bad} not")
     return 0 if bad == 0 else 1
 

@@ -29,9 +29,7 @@
 //       is summed in one-pass items dealt to lane groups (any mix of lengths);
 //     - register: each step loads U frames per group into VGPRs, then parses /
 //       sums / reduces them one by one (frame u+1 in flight behind frame u);
-//     - lane: one lane per frame, whole frame (small frames);
-//     - LDS-DMA ring: each wave streams frames through R LDS slots filled by
-//       global_load_lds_dwordx4; R-1 steps stay in flight at no VGPR cost.
+//     - lane: one lane per frame, whole frame (small frames).
 // * Group partial sums reduce with DPP (row_shr / row_bcast) into the group's
 //   last lane.
 // * Stores (default_cfg): frames <= 128 B write each check in-line as its
@@ -62,7 +60,6 @@ namespace xsknf_gpu {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
-[[maybe_unused]] constexpr int kTile = 64;   // consecutive frames per wave tile (LDS-DMA kernel, A/B)
 constexpr int kHdrChunks = 7;    // window chunks 0..6 hold frame bytes [0, 97) at any 16-B phase
 constexpr int kSlotBytes = 128;  // register kernel: per-group LDS header window
 
@@ -402,13 +399,8 @@ __device__ __forceinline__ bool store_check_sector(const FrameRef &r, const Head
 // the step would cost ~60 VGPRs of occupancy for a rare case).
 constexpr uint32_t kPendTag = 0x80000000u;
 // kNoDefer (defer_min_len: every check in-line): checksummer_internal.h
-#ifndef XSKNF_DEFER_MIN_LEN
-#define XSKNF_DEFER_MIN_LEN 1024
-#endif
-#ifndef XSKNF_DEFER_TILE_K   // a tile defers when K * (long frames) >= live frames (0: every long frame defers)
-#define XSKNF_DEFER_TILE_K 2
-#endif
-constexpr uint32_t kDeferMinLen = XSKNF_DEFER_MIN_LEN;        // hybrid default (tools/tune.py: 64 B, 570 B
+constexpr uint32_t kDeferTileK = 2;   // a tile defers when K * (long frames) >= live frames
+constexpr uint32_t kDeferMinLen = 1024;        // hybrid default (tools/tune.py: 64 B, 570 B
                                                // and IMIX prefer in-line, 1500 B deferred)
 
 // Result word of a frame after its pass-0 sum P0 (group-reduced, last lane).
@@ -489,11 +481,7 @@ __device__ __forceinline__ uint32_t store_result(const KernelArgs &a, uint32_t f
   if (valid) {
     XSKNF_GST(a.verdicts + f, 4) a.verdicts[f] = v;
   }
-#ifdef XSKNF_RECORD_PATH
-  if (!a.count_records && !a.tail_scatter) return 0;
-#else
   if (!a.count_records) return 0;
-#endif
   return static_cast<uint32_t>(__builtin_popcountll(
       __builtin_amdgcn_ballot_w64(valid && (static_cast<uint32_t>(v) & kRecTagMask) == kRecTag)));
 }
@@ -628,7 +616,7 @@ __device__ __forceinline__ void group_tiles(const KernelArgs &args, uint32_t blk
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(lane < T && tf0 + lane < args.n && dnext.z >= args.defer_min_len)));
       const uint32_t nlive = min(static_cast<uint32_t>(T), args.n - tf0);
-      if (XSKNF_DEFER_TILE_K > 0 && XSKNF_DEFER_TILE_K * nlong < nlive) ta.defer_min_len = kNoDefer;
+      if (kDeferTileK * nlong < nlive) ta.defer_min_len = kNoDefer;
     }
     dnext = *reinterpret_cast<const uint4 *>(args.descs + min((tile + waves) * T + min(lane, T - 1), last));
 
@@ -687,15 +675,11 @@ constexpr int kLaneSlot = 16 * kHdrChunks;   // per-lane LDS header window
 // issues 4 load instructions of a 5-chunk window, not 5 (the fifth re-read
 // the fourth chunk: one more instruction's worth of requests per frame), and a
 // step with frames at odd starts still loads its 5 chunks at once.
-// XSKNF_LANE_CLAMP=1 (A/B): every chunk loaded, as before.
-#ifndef XSKNF_LANE_CLAMP
-#define XSKNF_LANE_CLAMP 0
-#endif
 template <int NCH>
 __device__ __forceinline__ void load_lane(const FrameRef &r, uint4 (&v)[NCH]) {
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
-    if (XSKNF_LANE_CLAMP || k < 4 || __builtin_amdgcn_ballot_w64(k < r.nch))
+    if (k < 4 || __builtin_amdgcn_ballot_w64(k < r.nch))
       v[k] = *XSKNF_GLD(r.cp + min(k, r.nch - 1), 16);
     else
       v[k] = make_uint4(0, 0, 0, 0);   // past every frame of the step: outside every sum and parse
@@ -818,9 +802,6 @@ __device__ __forceinline__ LaneOut process_lane(const KernelArgs &args, const Fr
   return out;
 }
 
-#ifndef XSKNF_LANE_WT   // 0 (A/B): every in-line sector non-temporal
-#define XSKNF_LANE_WT 1
-#endif
 // One 16-byte piece of an in-line check sector: non-temporal, or (wt) sc1 nt,
 // written through the XCD's L2 at once.  Frames 2 KiB apart (the aligned
 // UMEM) share no line, and there the write-through store leaves no dirty line
@@ -945,7 +926,7 @@ void checksum_kernel_lane(const KernelArgs args) {
     r[0] = lane_ref(args, d[0], tf0 + lane);
     bool tl = TLM == 1;
     bool wt = false;   // in-line sectors written through (store_sector16)
-    if constexpr (TLM == 2 || XSKNF_LANE_WT) {
+    {
       // the tile's first and last frames' offsets: 64 frames packed back to back
       // span a few KiB, 64 chunks of a 2 KiB-chunk UMEM 126 KiB
       const uint64_t off = reinterpret_cast<uintptr_t>(r[0].fp) - reinterpret_cast<uintptr_t>(args.umem);
@@ -955,7 +936,7 @@ void checksum_kernel_lane(const KernelArgs args) {
                           static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<int>(off >> 32), kWave - 1)) << 32;
       const bool apart = (o1 > o0 ? o1 - o0 : o0 - o1) >= static_cast<uint64_t>(kWave - 1) * 256;
       if constexpr (TLM == 2) tl = apart;
-      wt = XSKNF_LANE_WT && apart;
+      wt = apart;
     }
     if (tl) load_lane_tl<NCH>(r[0], v[0]); else load_lane<NCH>(r[0], v[0]);
 #pragma unroll
@@ -1148,156 +1129,6 @@ struct ItemStage {
   }
 };
 
-// Phase B with LDS-DMA (split kernel, DMA = true): the same stages, but each
-// chunk goes straight into LDS (global_load_lds_dwordx4 ... nt: 64 lanes x 16 B
-// land contiguously at M0, lane l's at M0 + 16 l) instead of into VGPRs, and is
-// read back by the lane that requested it.  The two stages live in the wave's
-// header-window slots, dead after phase A when every check is deferred (the
-// only mode this variant runs in).  No stage registers: the kernel fits 4 waves
-// per SIMD at the 2-stage depth the register variant holds in 3.
-// (the s_nop: an SALU write of M0 needs one wait state before an LDS-DMA reads it)
-__device__ __forceinline__ void gload_lds_nt_asm(gchunk_ptr p, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(p), "s"(lds) : "memory", "m0");
-}
-
-__device__ __forceinline__ void gload_lds_asm(gchunk_ptr p, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(lds) : "memory", "m0");
-}
-
-template <int U, int NCH>
-struct ItemStageDMA {
-  Payload pl[U];
-  uint32_t fi[U];
-  int c0[U];
-  bool ok[U];
-  uint32_t buf;   // this stage's LDS: U * NCH KiB (wave-uniform)
-
-  template <int W, int LPF, int SPAN>
-  __device__ __forceinline__ void issue(uint32_t area, uint32_t mt, uint32_t it0, uint32_t total, int grp, int gl) {
-    constexpr int G = kWave / LPF;
-#pragma unroll
-    for (int q = 0; q < U; ++q) {
-      const uint32_t it = it0 + q * G + grp;
-      ok[q] = it < total;
-      const uint32_t e = lds_u16(area + 2 * min(it, total - 1));
-      fi[q] = e >> 8;
-      pl[q] = payload_of(lds_u128(mt + 16 * fi[q]));
-      c0[q] = W + static_cast<int>(e & 0xff) * SPAN;
-      if (!ok[q]) pl[q].hi = pl[q].lo;   // masked: sums nothing
-    }
-#pragma unroll
-    for (int q = 0; q < U; ++q)
-#pragma unroll
-      for (int k = 0; k < NCH; ++k)
-        gload_lds_nt_asm(pl[q].cp + min(c0[q] + k * LPF + gl, pl[q].nch - 1),
-                         __builtin_amdgcn_readfirstlane(buf + 1024 * (q * NCH + k)));
-  }
-
-  template <int N>
-  __device__ __forceinline__ void wait() {
-    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx950");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-  }
-
-  template <int LPF>
-  __device__ __forceinline__ void consume(uint32_t ab, int gl) {
-    wait<U * NCH>();   // the other stage's DMAs stay in flight
-    const uint32_t me = buf + 16 * static_cast<uint32_t>(lane_id());
-#pragma unroll
-    for (int q = 0; q < U; ++q) {
-      uint32_t blo = 0, bhi = 0;
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        const uint4 v = lds_u128(me + 1024 * (q * NCH + k));
-        chunk_sum_fast(v, (c0[q] + k * LPF + gl) * 16, pl[q].lo, pl[q].hi, pl[q].wl, pl[q].wh, blo, bhi);
-      }
-      const uint32_t P = group_sum_last<LPF>(blo + (bhi << 8));
-      if (gl == LPF - 1 && ok[q]) lds_add_u32(ab + 4 * fi[q], P);
-    }
-  }
-};
-
-#ifdef XSKNF_RECORD_PATH
-// Debug only (`make guard-rec`, DESIGN 3 "The intermittent fault"): the record
-// path removed from the product in round 2, kept compilable so that the guard
-// build can run it.  A static-schedule wave's tiles past its patch list park
-// check records in `verdicts`; after its list the wave reads them back, then
-// their descriptors, then the sectors, and rewrites each sector whole.
-__device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t tile0, uint32_t waves, int lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int piece = lane & 3;
-  constexpr int T = 2;
-  for (uint32_t tb = tile0; tb * kWave < args.n; tb += T * waves) {
-    uint32_t r[T];
-    bool rec[T];
-    uint64_t any = 0;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const uint32_t f = (tb + t * waves) * kWave + lane;
-      r[t] = f < args.n ? __builtin_nontemporal_load(XSKNF_GLD(reinterpret_cast<const uint32_t *>(args.verdicts) + f, 4))
-                        : 0u;
-    }
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      rec[t] = (r[t] & kRecTagMask) == kRecTag;
-      any |= __builtin_amdgcn_ballot_w64(rec[t]);
-    }
-    if (!any) continue;
-    uint32_t rr[T][4];
-    xsknf_gpu_desc d[T][4];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const uint32_t tile = tb + t * waves;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int src = 16 * k + (lane >> 2);
-        rr[t][k] = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(r[t])));
-        d[t][k] = *XSKNF_GLD(args.descs + min(tile * kWave + src, args.n - 1), 16);
-      }
-    }
-    uint4 v[T][4];
-    uint8_t *mine[T][4];
-    int o[T][4];
-    bool whole[T][4], has[T][4];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        has[t][k] = (rr[t][k] & kRecTagMask) == kRecTag;
-        uint8_t *fp = args.umem + umem_offset(d[t][k].addr);
-        uint8_t *chk = fp + ((rr[t][k] >> 16) & 0x7f) + 6;
-        uint8_t *sec = chk - (reinterpret_cast<uintptr_t>(chk) & 63);
-        whole[t][k] = has[t][k] && sec >= fp && sec + 64 <= fp + d[t][k].len &&
-                      (reinterpret_cast<uintptr_t>(chk) & 63) != 63;
-        mine[t][k] = whole[t][k] ? sec + 16 * piece : chk;
-        o[t][k] = static_cast<int>(chk - mine[t][k]);
-        if (whole[t][k]) v[t][k] = load_nt(reinterpret_cast<const uint4 *>(mine[t][k]));
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint16_t c = static_cast<uint16_t>(rr[t][k]);
-        if (whole[t][k]) {
-          uint4 w = put_byte(v[t][k], o[t][k], c);
-          w = put_byte(w, o[t][k] + 1, c >> 8);
-          store_nt16(mine[t][k], w);
-        } else if (has[t][k] && piece == 0) {
-          XSKNF_GST(mine[t][k], 2) {
-            mine[t][k][0] = static_cast<uint8_t>(c);
-            mine[t][k][1] = static_cast<uint8_t>(c >> 8);
-          }
-        }
-      }
-      if (rec[t]) {
-        int32_t *vp = args.verdicts + (tb + t * waves) * kWave + lane;
-        XSKNF_GST(vp, 4) *vp = args.fwd_verdict;
-      }
-    }
-  }
-}
-#endif
 
 // The patch list: where the default shape (W = 8, two items in flight: 157
 // VGPRs, 3 waves per SIMD, so 3 blocks per CU) has LDS to spare, a deferred
@@ -1314,40 +1145,22 @@ __device__ __forceinline__ void tail_scatter(const KernelArgs &args, uint32_t ti
 // written in-line; launches past their lists faulted with an illegal address
 // three times in full GPU suites, twice with the records and once in-line,
 // never alone or under the guard build.
-#ifndef XSKNF_PATCH_TILES
-#define XSKNF_PATCH_TILES 6
-#endif
-#ifndef XSKNF_PATCH_T
-#define XSKNF_PATCH_T 2
-#endif
-constexpr int kPatchTiles = XSKNF_PATCH_TILES;   // 6 x 64 x 8 B x 4 waves = 12 KiB per block
-constexpr int kPatchT = XSKNF_PATCH_T;           // tiles whose sectors are in flight together (3, 4: no gain, r02 ab_tail2)
-constexpr uint32_t kPatchValid = 1u << 23, kPatchWhole = 1u << 22, kPatchInWin = 1u << 24;   // + window offset / 16 << 25
-#ifndef XSKNF_PATCH_LAST_SLOT
-#define XSKNF_PATCH_LAST_SLOT 0
-#endif
-constexpr bool kPatchLastSlot = XSKNF_PATCH_LAST_SLOT;   // the wave's last tile: sectors from its window slots
+constexpr int kPatchTiles = 6;   // 6 x 64 x 8 B x 4 waves = 12 KiB per block
+constexpr int kPatchT = 2;       // tiles whose sectors are in flight together (3, 4: no gain, r02 ab_tail2, r04)
+// entry flags; kPatchInWin + window offset / 16 << 25 say where the sector lies
+// in the frame's header window (round 4 took such sectors from the slots
+// instead of reading them again: no gain, removed in round 5)
+constexpr uint32_t kPatchValid = 1u << 23, kPatchWhole = 1u << 22, kPatchInWin = 1u << 24;
 constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with margin)
 
 // Tiles in a wave's patch list: 16 x 2 items fit 3 waves per SIMD (6 tiles per
 // wave at 1M frames; 7 with the pool, whose faster waves take more units), 16 x
-// 3 fit 2 (8 tiles per wave); the other shapes keep no list.
-// The compact shape (A/B: W = 8, 16 x 2, one item in flight, 4-wave blocks)
-// fits 4 waves per SIMD by registers (<= 128 VGPRs) and 4 blocks per CU by
-// LDS: its phase-B scratch (item queue, frame meta, accumulators) lives in the
-// wave's window slots, dead once phase A has read them (every check deferred),
-// and its list holds 4 tiles (4 x 64 x 8 B): 40 KiB per block.
-// A block of more than 4 waves holds a whole CU's waves and shares the CU's
-// tiles as a pool; XSKNF_BIG_STATIC (A/B) deals them statically instead.
-#ifndef XSKNF_BIG_STATIC
-#define XSKNF_BIG_STATIC 0
-#endif
-constexpr bool pooled_split(int sw) { return sw > kWavesPerBlock && !XSKNF_BIG_STATIC; }
-
-template <int W, int NCH, int U, bool DMA, bool PFW, bool kPool>
-constexpr bool compact_split() {
-  return W == 8 && NCH == 2 && U == 1 && !DMA && !PFW && !kPool;
-}
+// 3 fit 2 (8 tiles per wave); the other shapes keep no list.  A block of more
+// than 4 waves holds a whole CU's waves and shares the CU's tiles as a pool.
+// (Round 4's compact shape -- 4 waves per SIMD, phase-B scratch in the dead
+// window slots, 4-tile lists -- and its 16-wave static twin tied the default
+// and were removed in round 5: DESIGN 7.)
+constexpr bool pooled_split(int sw) { return sw > kWavesPerBlock; }
 
 // The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
 // a 16-unit list (64 KiB of its block's 135 KiB): with every check deferred
@@ -1356,11 +1169,10 @@ constexpr bool compact_split() {
 // 1457.2-1458.1 vs 1461.6-1462.9 on a second box, NIC checks -4 us;
 // profiles/r05/ab/).
 constexpr int kJumboPatchUnits = 16;
-template <int W, int NCH, int U, bool DMA, bool PFW, bool kPool>
+template <int W, int NCH, int U, bool kPool>
 constexpr int patch_list_tiles() {
-  if constexpr (compact_split<W, NCH, U, DMA, PFW, kPool>()) return 4;
-  if constexpr (W == 4 && NCH == 3 && U >= 2 && kPool && !DMA && !PFW) return kJumboPatchUnits;
-  return (W == 8 && U >= 2 && !DMA && !PFW) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
+  if constexpr (W == 4 && NCH == 3 && U >= 2 && kPool) return kJumboPatchUnits;
+  return (W == 8 && U >= 2) ? (NCH == 2 ? (kPool ? 7 : kPatchTiles) : 8) : 0;
 }
 
 __device__ __forceinline__ uint2 patch_entry(const KernelArgs &a, const FrameRef &r, int u, uint16_t c, int wbytes) {
@@ -1392,11 +1204,7 @@ __device__ __forceinline__ uint2 lds_u64(uint32_t a) {
 // round, 4 lanes per frame, each frame's sector read and rewritten whole (one
 // non-temporal 64-byte store of 4 lanes), or its 2 check bytes where the sector
 // leaves the frame.  kPatchT tiles' sectors are in flight together.
-// last_slots: the LDS slots (stride `kslot`) still hold the windows of tile
-// ntiles - 1, the wave's last (kPatchLastSlot): its in-window sectors are taken
-// from there instead of being read again.
-__device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t pl, int ntiles, int lane,
-                                                bool last_in_slots, uint32_t area, uint32_t kslot) {
+__device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t pl, int ntiles, int lane) {
   const int piece = lane & 3;
   uint8_t *const base = args.umem - (reinterpret_cast<uintptr_t>(args.umem) & 63);   // keeps global addressing
   constexpr int T = kPatchT;
@@ -1413,9 +1221,7 @@ __device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t
         uint8_t *sec = base + (static_cast<uint64_t>(e.x) << 6);
         const bool whole = (e.y & (kPatchValid | kPatchWhole)) == (kPatchValid | kPatchWhole);
         mine[t][k] = whole ? sec + 16 * piece : sec + ((e.y >> 16) & 63);
-        if (kPatchLastSlot && last_in_slots && t0 + t == ntiles - 1 && (e.y & kPatchInWin))
-          v[t][k] = lds_u128(area + kslot * (16 * k + (lane >> 2)) + 16 * ((e.y >> 25) & 7) + 16 * piece);
-        else if (whole)
+        if (whole)
           v[t][k] = load_nt(reinterpret_cast<const uint4 *>(mine[t][k]));
       }
     }
@@ -1444,11 +1250,10 @@ __device__ __forceinline__ void tail_patch_list(const KernelArgs &args, uint32_t
 // One item per group in flight (U = 1) fits 4 waves per SIMD (<= 128 VGPRs),
 // which the LDS footprint also allows (4 blocks per CU): measured IMIX / 570 B
 // +8-11 % from 2 -> 3 waves per SIMD, so the register budget is pinned.
-template <int W, int LPF, int NCH, int U, bool TL, bool DMA, bool PFW, int SW>
-__global__ __launch_bounds__(SW * kWave) __attribute__((amdgpu_waves_per_eu(U == 1 || DMA ? 4 : 1)))
+template <int W, int LPF, int NCH, int U, bool TL, int SW>
+__global__ __launch_bounds__(SW * kWave) __attribute__((amdgpu_waves_per_eu(U == 1 ? 4 : 1)))
 void checksum_kernel_split(const KernelArgs args) {
   static_assert(W >= 4 && (W <= kHdrChunks || W == 8), "header window");
-  static_assert(!PFW || (TL && !DMA && W == 8), "window prefetch: the transposed W = 8 layout, register phase B");
   static_assert(!TL || W == 4 || W == 8, "transposed window load: W lanes x 16 B per frame");
   static_assert(kWave % LPF == 0 && LPF >= 4, "group shape");
   constexpr int G = kWave / LPF;
@@ -1458,22 +1263,13 @@ void checksum_kernel_split(const KernelArgs args) {
   constexpr int kItemCap = 256;                            // items per round of phase B
   constexpr uint32_t kItemsPerFrame = 255;                 // u8 pass index; more: whole-wave loop
   constexpr bool kPool = pooled_split(SW);   // one block per CU: its waves share the CU's tiles
-  constexpr bool kCompact = compact_split<W, NCH, U, DMA, PFW, kPool>();
-  constexpr int kScratch = kCompact ? 1 : kWave;   // phase-B scratch of its own (else in the slots)
-  // Phase C's in-line sector stores take the sector from the lane's window
-  // slot, which phase B has overwritten where it keeps its stages (DMA), the
-  // next tile's windows (PFW) or its scratch (kCompact) there: those shapes
-  // store a phase-C check as its 2 bytes.  (With every check deferred they
-  // store none in-line, except past the patch list -- the DMA and PFW shapes
-  // keep no list, so with tail patches asked for all of theirs are in-line.)
-  constexpr bool kSlotsLiveInC = !kCompact && !DMA && !PFW;
   __shared__ __attribute__((aligned(16))) uint8_t slots[SW][kSlotArea];
-  __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kCompact ? 1 : kItemCap];
-  __shared__ __attribute__((aligned(16))) uint4 meta[SW][kScratch];
-  __shared__ __attribute__((aligned(16))) uint32_t accb[SW][kScratch];
+  __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kItemCap];
+  __shared__ __attribute__((aligned(16))) uint4 meta[SW][kWave];
+  __shared__ __attribute__((aligned(16))) uint32_t accb[SW][kWave];
   // (jumbo's 16-unit list: each wave patching its own list after its last unit tied the scatter
   // pass, 1463 vs 1461 us -- profiles/r02/ab_jumbo_tail.jsonl; from the block's queue it is ahead)
-  constexpr int PT = patch_list_tiles<W, NCH, U, DMA, PFW, kPool>();
+  constexpr int PT = patch_list_tiles<W, NCH, U, kPool>();
   __shared__ __attribute__((aligned(16))) uint2 plist[SW][PT > 0 ? PT * kWave : 1];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -1481,20 +1277,15 @@ void checksum_kernel_split(const KernelArgs args) {
   const int grp = lane / LPF, gl = lane % LPF;
   const uint32_t area = lds_addr(&slots[wv][0]);
   const uint32_t slot = area + kSlot * lane;
-  static_assert(!kCompact || 16 * kWave + 4 * kWave + 2 * kItemCap <= kSlotArea, "scratch in the slots");
-  const uint32_t mt = kCompact ? area : lds_addr(&meta[wv][0]);
-  const uint32_t ab = kCompact ? area + 16 * kWave : lds_addr(&accb[wv][0]);
-  const uint32_t iq = kCompact ? area + 20 * kWave : lds_addr(&itemq[wv][0]);
+  const uint32_t mt = lds_addr(&meta[wv][0]);
+  const uint32_t ab = lds_addr(&accb[wv][0]);
+  const uint32_t iq = lds_addr(&itemq[wv][0]);
   const uint32_t waves = gridDim.x * SW;
   const uint32_t last = args.n - 1;
 // Streaming waves issue ahead of patching ones: priority 1 until the wave's
 // last unit, 0 for its patches (with the patch queue below: 1500 B -0.9..-1.5
-// us, its NIC traffic -3 us, other sizes level -- profiles/r04/ab/ab_patch_prio_*;
-// XSKNF_PATCH_PRIO=0 for the A/B)
-#ifndef XSKNF_PATCH_PRIO
-#define XSKNF_PATCH_PRIO 1
-#endif
-  if (XSKNF_PATCH_PRIO) __builtin_amdgcn_s_setprio(1);
+// us, its NIC traffic -3 us, other sizes level -- profiles/r04/ab/ab_patch_prio_*)
+  __builtin_amdgcn_s_setprio(1);
 
   uint32_t nrec = 0;
 #ifdef XSKNF_TIMELINE
@@ -1533,12 +1324,10 @@ void checksum_kernel_split(const KernelArgs args) {
   // kParts parts each, so the waves' streams end closer together: halves up to
   // 4 KiB (quarters there: 570 B 165 vs 151 us, 1024 B 213 vs 205 --
   // profiles/r02/ab_pool.jsonl), quarters for jumbo tiles (W = 4), which
-  // stream for ~160 us each.  XSKNF_POOL_HALVES=0 (A/B): whole tiles only.
-#ifndef XSKNF_POOL_HALVES
-#define XSKNF_POOL_HALVES 1
-#endif
+  // stream for ~160 us each.  (Whole tiles only: IMIX level, 1500 B +6-7 us;
+  // profiles/r04/ab/ab_pool_no_halves*.)
   constexpr uint32_t kParts = W == 4 ? 4u : 2u;
-  const uint32_t nsplit = kPool && XSKNF_POOL_HALVES ? min(bt, static_cast<uint32_t>(SW)) : 0u;
+  const uint32_t nsplit = kPool ? min(bt, static_cast<uint32_t>(SW)) : 0u;
   const uint32_t nfull = bt - nsplit;
   const uint32_t units = nfull + kParts * nsplit;
   const auto pool_unit = [&](uint32_t p) { return p < units ? p : kNoTile; };
@@ -1570,9 +1359,6 @@ void checksum_kernel_split(const KernelArgs args) {
     tn = t0 + waves < ntiles ? t0 + waves : kNoTile;
     tnn = t0 + 2 * waves < ntiles ? t0 + 2 * waves : kNoTile;
   }
-#ifndef XSKNF_PATCH_SHARED
-#define XSKNF_PATCH_SHARED 1
-#endif
   // One patch queue per block (the pooled shapes) instead of each wave patching its own list
   // after its last unit: a wave publishes each finished unit's list (its index,
   // or a null mark for a unit with nothing to patch), and a wave whose stream
@@ -1582,32 +1368,21 @@ void checksum_kernel_split(const KernelArgs args) {
   // units is known, so the consumers' loop ends; the wait for a mark is bounded
   // by the clock.  Measured alone: 1500 B -0.8..-1.5 us, the launch still ends
   // ~7 us after its last stream (profiles/r04/ab/ab_patch_queue_*); with the
-  // streaming waves' priority (XSKNF_PATCH_PRIO) the product's since round 4.
-  // XSKNF_PATCH_SHARED=0: each wave patches its own list (A/B).
-#ifndef XSKNF_PATCH_SHARED_STATIC   // (A/B) the queue in the static 4-wave blocks too (alone: IMIX +1 us)
-#define XSKNF_PATCH_SHARED_STATIC 0
-#endif
-  constexpr bool kShared = XSKNF_PATCH_SHARED && PT > 0 && (kPool || XSKNF_PATCH_SHARED_STATIC);
+  // streaming waves' priority the product's since round 4.  The static 4-wave
+  // blocks (IMIX) keep each wave patching its own list (a queue there: IMIX +1
+  // us, profiles/r04/ab/ab_patch_queue_static_bench.jsonl).
+  constexpr bool kShared = PT > 0 && kPool;
   constexpr uint32_t kPQ = kShared ? SW * PT : 1;   // marks: the grid is sized so a block has <= SW * PT units
   constexpr uint32_t kPQNull = 0xffffu;
   __shared__ uint32_t pq_tail, pq_head;
   __shared__ uint32_t pq[kPQ];
-  __shared__ uint32_t pq_last[kShared ? SW : 1];   // a wave's last unit, once it has no more (its slots hold it)
   const bool shared_on = kShared && list_ok;   // block-uniform
   bool pq_full = false;                        // wave-uniform: a mark found no room
   uint32_t block_units = 0;
   if constexpr (kShared) {
-    if constexpr (kPool) {
-      block_units = units;
-    } else {
-      for (int w = 0; w < SW; ++w) {
-        const uint32_t t0 = blockIdx.x * SW + w;
-        block_units += t0 < ntiles ? (ntiles - t0 + waves - 1) / waves : 0u;
-      }
-    }
+    block_units = units;
     if (threadIdx.x == 0) pq_tail = pq_head = 0;
     for (uint32_t i = threadIdx.x; i < kPQ; i += SW * kWave) pq[i] = 0;
-    if (threadIdx.x < SW) pq_last[threadIdx.x] = ~0u;
     __syncthreads();
   }
   const auto desc_of = [&](uint32_t t) {
@@ -1616,31 +1391,6 @@ void checksum_kernel_split(const KernelArgs args) {
   // descriptors travel two tiles ahead (static), one unit ahead (kPool)
   uint4 d = desc_of(tile);
   uint4 dn = kPool ? d : desc_of(tn);
-  // PFW: the next tile's header windows go straight into the slots by LDS-DMA
-  // as soon as this tile's phase A is done with them (every check deferred: the
-  // slots are dead until then), so a tile starts on windows already in LDS.
-  // The transposed layout is the DMA's own: instruction p lands 64 x 16 B at
-  // area + 1 KiB p (kSlot = 16 W = 128: frame 8p + lane / 8, piece lane % 8).
-  const auto window_dma = [&](const uint4 dd, uint32_t ff) {
-    const FrameRef rn = lane_ref(args, dd, ff);
-    const uintptr_t cpv = reinterpret_cast<uintptr_t>(rn.cp);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slots' last reads are done
-#pragma unroll
-    for (int p = 0; p < W; ++p) {
-      const int g = (kWave / W) * p + lane / W;
-      const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv)));
-      const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
-      const int nc = __builtin_amdgcn_ds_bpermute(g << 2, rn.nch);
-      const gchunk_ptr cp = reinterpret_cast<gchunk_ptr>((static_cast<uintptr_t>(hi) << 32) | lo);
-      gload_lds_asm(cp + min(lane % W, nc - 1), __builtin_amdgcn_readfirstlane(area + 1024 * p));
-    }
-  };
-  bool window_pending = false;
-  if constexpr (PFW) {
-    static_assert(!PFW || kSlot == 16 * W, "DMA layout = slot layout");
-    window_dma(d, unit_f0(tile) + lane);
-    window_pending = true;
-  }
   while (tile != kNoTile) {
     XSKNF_TL_START();
     if constexpr (kPool) {   // claim the next unit, and load its descriptors while this one streams
@@ -1658,11 +1408,7 @@ void checksum_kernel_split(const KernelArgs args) {
     const uint32_t f = lane < cnt ? f0 + lane : args.n;   // lanes past a half unit hold no frame
     const FrameRef r = lane_ref(args, d, f);
     uint4 v[W];
-    if constexpr (PFW) {
-      if (window_pending) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int k = 0; k < W; ++k) v[k] = lds_u128(slot + 16 * k);
-    } else if constexpr (TL) {
+    if constexpr (TL) {
       // transposed: lanes W*i .. W*i+W-1 load the window of frame (64/W)*p + i
       // (p = 0..W-1), one coalesced 16*W-byte request per frame instead of W
       // 16-byte ones, and drop it in that frame's slot
@@ -1694,16 +1440,12 @@ void checksum_kernel_split(const KernelArgs args) {
     // per-tile store policy, as the register kernel: long frames defer their
     // checks only where they are at least half of the tile
     // (a wave's tiles past its patch list: in-line)
-#ifdef XSKNF_RECORD_PATH
-    uint32_t defer_min = kPool && args.tail_scatter && !to_list ? kNoDefer : args.defer_min_len;
-#else
     uint32_t defer_min = args.tail_scatter && !to_list ? kNoDefer : args.defer_min_len;
-#endif
     if (defer_min != kNoDefer && defer_min != 0 && !args.no_scatter) {
       const uint32_t nlong = static_cast<uint32_t>(__builtin_popcountll(
           __builtin_amdgcn_ballot_w64(f < args.n && d.z >= defer_min)));
       const uint32_t nlive = f0 < args.n ? min(cnt, args.n - f0) : 0u;
-      if (XSKNF_DEFER_TILE_K > 0 && XSKNF_DEFER_TILE_K * nlong < nlive) defer_min = kNoDefer;
+      if (kDeferTileK * nlong < nlive) defer_min = kNoDefer;
     }
 
     // ---- phase A: header, window sum, short frames finished ----
@@ -1761,10 +1503,6 @@ void checksum_kernel_split(const KernelArgs args) {
     }
     store_sectors(o, lane, args.plain_sector);
     const uint32_t part = h.pseudo + args.payload_mult * (PA - h.old_check);
-    if constexpr (PFW) {
-      window_pending = tn != kNoTile;
-      if (window_pending) window_dma(dn, unit_f0(tn) + lane);
-    }
 
     // ---- phase B: payload items of the longer frames ----
     XSKNF_TL_MARK(tl_p);
@@ -1788,15 +1526,7 @@ void checksum_kernel_split(const KernelArgs args) {
         for (uint32_t k = k0; __builtin_amdgcn_ballot_w64(k < k1); ++k)
           if (k < k1) lds_store_u16(iq + 2 * (start + k - r0), static_cast<uint16_t>((lane << 8) | k));
         compiler_barrier();
-        using Stage = typename std::conditional<DMA, ItemStageDMA<U, NCH>, ItemStage<U, NCH>>::type;
-        Stage sa, sb;
-        if constexpr (DMA) {
-          static_assert(!DMA || 2 * U * NCH * 1024 <= kSlotArea, "two stages must fit the slot area");
-          sa.buf = area;
-          sb.buf = area + 1024 * U * NCH;
-          // the slots' last phase-A reads complete before the first DMA lands there
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
+        ItemStage<U, NCH> sa, sb;
         sa.template issue<W, LPF, SPAN>(iq, mt, 0, nr, grp, gl);
         for (uint32_t it0 = 0;;) {
           sb.template issue<W, LPF, SPAN>(iq, mt, it0 + G * U, nr, grp, gl);
@@ -1806,7 +1536,6 @@ void checksum_kernel_split(const KernelArgs args) {
           sb.template consume<LPF>(ab, gl);
           if ((it0 += G * U) >= nr) { sa.template wait<0>(); break; }
         }
-        window_pending = false;   // that wait<0> drained the window DMA too
       }
       // frames past the item budget: the whole wave sums each one
       for (uint64_t hm = __builtin_amdgcn_ballot_w64(huge); hm; hm &= hm - 1) {
@@ -1835,7 +1564,7 @@ void checksum_kernel_split(const KernelArgs args) {
         if (static_cast<uint32_t>(r.len) >= defer_min) {
           if (to_list) ent = patch_entry(args, r, h.u, c, 16 * W);
           else res = static_cast<int32_t>(kRecTag | (static_cast<uint32_t>(h.u) << 16) | c);
-        } else if (kSlotsLiveInC && args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 &&
+        } else if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 &&
                    sec >= c0 && sec + 64 <= c0 + 16 * W) {
           const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
           lds_store_u8(at, static_cast<uint8_t>(c));
@@ -1889,12 +1618,10 @@ void checksum_kernel_split(const KernelArgs args) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long tl1 = wall_clock64();
 #endif
-  if (XSKNF_PATCH_PRIO) __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_s_setprio(0);
   if (args.tail_scatter) {
     if constexpr (kShared) {
       if (shared_on) {
-        if (kPatchLastSlot && lane == 0 && it > 0)
-          __hip_atomic_store(&pq_last[wv], static_cast<uint32_t>(it - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint64_t tw0 = wall_clock64();
         for (;;) {
           uint32_t h = 0;
@@ -1911,21 +1638,12 @@ void checksum_kernel_split(const KernelArgs args) {
           if (m == 0) break;
           if (m != kPQNull) {
             const uint32_t w2 = (m - 1) >> 8, t2 = (m - 1) & 0xffu;
-            // kPatchLastSlot: the unit is its wave's last, so that wave's slots still hold its windows
-            const bool in_slots = kPatchLastSlot &&
-                t2 == static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
-                          __hip_atomic_load(&pq_last[w2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))));
-            tail_patch_list(args, lds_addr(&plist[w2][0]) + 8 * t2 * kWave, 1, lane, in_slots,
-                            lds_addr(&slots[w2][0]), kSlot);
+            tail_patch_list(args, lds_addr(&plist[w2][0]) + 8 * t2 * kWave, 1, lane);
           }
         }
       }
     }
-    if (any_entry && (!shared_on || pq_full)) tail_patch_list(args, pl, min(it, PT), lane, it <= PT, area, kSlot);
-#ifdef XSKNF_RECORD_PATH
-    if (!kPool && __builtin_amdgcn_readfirstlane(nrec))
-      tail_scatter(args, blockIdx.x * SW + wv + (list_ok ? PT : 0) * waves, waves, lane);
-#endif
+    if (any_entry && (!shared_on || pq_full)) tail_patch_list(args, pl, min(it, PT), lane);
   } else {
     publish_records(args, nrec, lane);
   }
@@ -1935,277 +1653,7 @@ void checksum_kernel_split(const KernelArgs args) {
 #endif
 }
 
-#ifdef XSKNF_AB
-// ---- small-frame kernel (A/B: frames of at most 64 B, BASELINE config 2) --------
-//
-// Occupancy over per-wave overlap: a frame of <= 64 B is one 64-byte sector at
-// a 2 KiB stride, so the step is bound by how many such sectors are in flight,
-// not by bytes.  Each wave takes a tile of 64 frames: its 4 window loads are
-// transposed (lanes 4i .. 4i+3 read frame 16p + i's four 16-byte chunks, one
-// coalesced 64-byte request per frame) into a 64-byte LDS slot per frame; lane
-// l then parses, sums and finishes frame l from its slot, patches its check into
-// the slot and the wave writes each check's sector back whole, 16 frames per
-// store (4 lanes each), right after reading it.  4 KiB of LDS and <= 64 VGPRs
-// per wave: 8 waves per SIMD.  Frames longer than the window read their other
-// chunks lane by lane (any length is correct; hint > 64 picks another kernel).
-// MODE (timing experiments only, wrong output): 1 = no parse / sum, the
-// loaded sector is written back as read; 2 = also no LDS: the window
-// registers are stored straight back (the hbm_probe in-stream shape).
-template <int SW, bool NT, int MODE = 0>
-__global__ __launch_bounds__(SW * kWave) __attribute__((amdgpu_waves_per_eu(8)))
-void checksum_kernel_small(const KernelArgs args) {
-  constexpr int kWin = 4;                               // window chunks (64 B)
-  __shared__ __attribute__((aligned(16))) uint8_t win[SW][kWave * 16 * kWin];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint32_t area = lds_addr(&win[wv][0]);
-  const uint32_t slot = area + 16 * kWin * lane;
-  const uint32_t waves = gridDim.x * SW;
-  const uint32_t last = args.n - 1;
-  const uint32_t ntiles = (args.n + kWave - 1) / kWave;
-  uint32_t tile = blockIdx.x * SW + wv;
-  const auto desc_at = [&](uint32_t t) {
-    return *XSKNF_GLD(reinterpret_cast<const uint4 *>(args.descs + (t < ntiles ? min(t * kWave + lane, last) : last)), 16);
-  };
-  uint4 d = desc_at(tile);
-  for (; tile < ntiles; tile += waves) {
-    const uint4 dn = desc_at(tile + waves);
-    const uint32_t f = tile * kWave + lane;
-    const FrameRef r = lane_ref(args, d, f);
-    // transposed window: instruction p, lane L -> chunk L % 4 of frame 16 p + L / 4
-    {
-      const uintptr_t cpv = reinterpret_cast<uintptr_t>(r.cp);
-      uint4 x[kWin];
-#pragma unroll
-      for (int p = 0; p < kWin; ++p) {
-        const int g = 16 * p + lane / 4;
-        const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv)));
-        const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
-        const int nc = __builtin_amdgcn_ds_bpermute(g << 2, r.nch);
-        const gchunk_ptr cp = reinterpret_cast<gchunk_ptr>((static_cast<uintptr_t>(hi) << 32) | lo);
-        if constexpr (NT) {
-          x[p] = load_nt(cp + min(lane % 4, nc - 1));
-        } else {
-          const u32x4 y = *XSKNF_GLD(cp + min(lane % 4, nc - 1), 16);
-          x[p] = make_uint4(y.x, y.y, y.z, y.w);
-        }
-      }
-      if constexpr (MODE == 2) {
-#pragma unroll
-        for (int p = 0; p < kWin; ++p) {
-          const int g = 16 * p + lane / 4;
-          const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv)));
-          const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(g << 2, static_cast<int>(cpv >> 32)));
-          uint8_t *cp = reinterpret_cast<uint8_t *>((static_cast<uintptr_t>(hi) << 32) | lo);
-          store_nt16(cp + 16 * (lane % 4), x[p]);
-        }
-        if (f < args.n) args.verdicts[f] = 0;
-        d = dn;
-        continue;
-      }
-      compiler_barrier();
-#pragma unroll
-      for (int p = 0; p < kWin; ++p) lds_store_u128(area + 16 * kWin * (16 * p + lane / 4) + 16 * (lane % 4), x[p]);
-      compiler_barrier();
-    }
-    if constexpr (MODE == 1) {
-      LaneOut o1 = {0, r.live && r.rs == 0 && r.len >= 64, slot, r.fp};
-      store_sectors(o1, lane, false);
-      if (f < args.n) args.verdicts[f] = 0;
-      compiler_barrier();
-      d = dn;
-      continue;
-    }
-    // header: every field but the UDP length / old check lies in the window
-    // (rs <= 15); those 4 bytes come from the frame itself when the header is
-    // longer than the window (large ihl)
-    const uint32_t hb = slot + r.rs;
-    Header h;
-    {
-      const uint32_t w12 = lds_u32(hb + 12), w20 = lds_u32(hb + 20), w24 = lds_u32(hb + 24);
-      const uint32_t w28 = lds_u32(hb + 28), w32 = lds_u32(hb + 32);
-      h.u = 14 + 4 * ((w12 >> 16) & 0x0f);
-      uint32_t wu = 0;
-      if (r.rs + h.u + 8 <= 16 * kWin) {
-        wu = lds_u32(hb + h.u + 4);
-      } else if (r.live && h.u + 8 <= r.len) {
-        const uint8_t *q = XSKNF_GLD(r.fp + h.u + 4, 4);
-        wu = q[0] | (static_cast<uint32_t>(q[1]) << 8) | (static_cast<uint32_t>(q[2]) << 16) |
-             (static_cast<uint32_t>(q[3]) << 24);
-      }
-      h.ipv4 = (w12 & 0xffffu) == 0x0008u;
-      h.udp = (w20 >> 24) == 17u;
-      h.pseudo = (w24 >> 16) + (w28 & 0xffffu) + (w28 >> 16) + (w32 & 0xffffu) + 0x1100u + (wu & 0xffffu);
-      h.old_check = wu >> 16;
-    }
-    bool do_sum;
-    const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
-    LaneOut o = {r.exists ? verdict : 0, false, slot, r.fp};
-    if (do_sum) {
-      const int lo = r.rs + h.u, hi = r.rs + r.len;
-      const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
-      const uint32_t wh = wl << 8 | wl >> 24;
-      uint32_t acc_lo = 0, acc_hi = 0;
-#pragma unroll
-      for (int k = 0; k < kWin; ++k) chunk_sum(lds_u128(slot + 16 * k), 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
-      for (int k = kWin; k < r.nch; ++k)
-        chunk_sum(*XSKNF_GLD(r.cp + k, 16), 16 * k, lo, hi, wl, wh, acc_lo, acc_hi);
-      const uint16_t c = check_of(h, acc_lo + (acc_hi << 8), args.payload_mult);
-      const uintptr_t f0 = reinterpret_cast<uintptr_t>(r.fp);
-      const uintptr_t ck = f0 + h.u + 6;
-      const uintptr_t sec = ck & ~static_cast<uintptr_t>(63);
-      const uintptr_t c0 = reinterpret_cast<uintptr_t>(r.cp);
-      if (!check_changes(args, h, c)) {
-        // the frame already holds c
-      } else if (args.sector_stores && sec >= f0 && sec + 64 <= f0 + r.len && (ck & 63) != 63 && sec >= c0 &&
-          sec + 64 <= c0 + 16 * kWin) {
-        const uint32_t at = slot + static_cast<uint32_t>(ck - c0);
-        lds_store_u8(at, static_cast<uint8_t>(c));
-        lds_store_u8(at + 1, static_cast<uint8_t>(c >> 8));
-        o.sector = true;
-        o.lds_sec = slot + static_cast<uint32_t>(sec - c0);
-        o.gsec = r.fp + static_cast<intptr_t>(sec - f0);
-      } else {
-        XSKNF_GST(r.fp + h.u + 6, 2) *reinterpret_cast<uint16_t *>(r.fp + h.u + 6) = c;   // :108
-      }
-    }
-    store_sectors(o, lane, args.plain_sector);
-    if (f < args.n) {
-      XSKNF_GST(args.verdicts + f, 4) args.verdicts[f] = o.res;
-    }
-    compiler_barrier();   // the next tile rewrites the slots
-    d = dn;
-  }
-}
-#endif  // XSKNF_AB
 
-#ifdef XSKNF_AB
-// ---- LDS-DMA ring kernel ------------------------------------------------------
-//
-// Each wave streams its steps (G frames, one per group) through a private ring
-// of R LDS slots filled by global_load_lds_dwordx4 (16 B per lane straight into
-// LDS).  At step j the wave issues the DMA of step j+R-1, then waits -- with an
-// explicitly counted vmcnt -- only for step j's slot.  The DMA is issued from
-// inline asm because the compiler drains vmcnt to 0 before every LDS read once
-// it sees an LDS-DMA in flight; the waits count only this wave's DMAs younger
-// than the slot being read (other vector-memory operations can only make such
-// a wait stricter, never too weak).  Before a slot is refilled, every read of
-// it has been consumed (its data fed the previous step's reduction).
-//
-// Slot layout: DMA instruction k of a step writes 1 KiB at slot + k*1024, lane l
-// at +16*l: group g's chunk c = k*LPF + gl sits at slot + k*1024 + 16*(g*LPF + gl),
-// and the frame's chunks 0..LPF-1 (every header byte for LPF >= 8) are
-// contiguous at slot + 16*g*LPF.
-
-__device__ __forceinline__ void dma16_nt(const void *gaddr, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
-               :: "v"(gaddr), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory", "m0");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx950");
-  asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
-}
-
-template <int LPF, int NCH, int R>
-__global__ __launch_bounds__(kBlock) void checksum_kernel_dma(const KernelArgs args) {
-  static_assert(kWave % LPF == 0 && LPF >= 8, "header window must sit in chunk slot k = 0");
-  static_assert(R >= 2 && R <= 4 && (R - 1) * NCH < 64, "ring depth / vmcnt range");
-  constexpr int G = kWave / LPF;
-  constexpr int SLOT = NCH * 1024;
-  constexpr int SPT = kTile / G;             // steps per tile
-  static_assert(SPT >= 2 * R - 1, "a tile's descriptor DMA lands before its first frame DMA");
-
-  __shared__ __attribute__((aligned(1024))) uint8_t ring[kWavesPerBlock][R][SLOT];
-  __shared__ __attribute__((aligned(16))) int32_t recs[kWavesPerBlock][kTile];
-  __shared__ __attribute__((aligned(16))) uint32_t parts[kWavesPerBlock][kTile];
-  __shared__ __attribute__((aligned(1024))) xsknf_gpu_desc dtile[kWavesPerBlock][2][kTile];
-
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int grp = lane / LPF;
-  const int gl = lane % LPF;
-  const uint32_t ring0 = lds_addr(&ring[wv][0][0]);
-  const uint32_t rec = lds_addr(&recs[wv][0]);
-  const uint32_t part = lds_addr(&parts[wv][0]);
-  const uint32_t dsc0 = lds_addr(&dtile[wv][0][0]);
-  const uint32_t waves = gridDim.x * kWavesPerBlock;
-  const uint32_t wg = blockIdx.x * kWavesPerBlock + wv;
-  const uint32_t last = args.n - 1;
-
-  // Step j of this wave covers tile k = j / SPT (global tile wg + k*waves),
-  // frames (j % SPT)*G + grp of it.  Tile k's descriptors sit in dtile[k & 1],
-  // DMA'd when tile k-1 starts (tile 0 and 1 in the prologue).
-  auto tile_f0 = [&](uint32_t k) -> uint32_t { return (wg + k * waves) * kTile; };
-  auto dma_descs = [&](uint32_t k) {
-    dma16_nt(args.descs + min(tile_f0(k) + lane, last), dsc0 + (k & 1) * (kTile * 16));
-  };
-  auto ref_of_step = [&](uint32_t j) -> FrameRef {
-    const uint32_t i = (j % SPT) * G + grp;
-    return ref_from_lds(args, dsc0 + ((j / SPT) & 1) * (kTile * 16) + 16 * i, tile_f0(j / SPT) + i);
-  };
-  auto issue = [&](const FrameRef &r, int s) {
-#pragma unroll
-    for (int k = 0; k < NCH; ++k) dma16_nt(r.cp + min(k * LPF + gl, r.nch - 1), ring0 + s * SLOT + k * 1024);
-  };
-
-  dma_descs(0);
-  dma_descs(1);
-  wait_vmcnt<1>();                      // tile 0's descriptors
-  FrameRef ref[R];
-#pragma unroll
-  for (int j = 0; j < R - 1; ++j) {
-    ref[j] = ref_of_step(j);
-    issue(ref[j], j);
-  }
-
-  uint32_t j = 0;
-  uint32_t nrec = 0;                    // records this wave parked (wave-uniform)
-  while (true) {
-#pragma unroll
-    for (int s = 0; s < R; ++s) {       // unrolled so ring slots and refs are static
-      const uint32_t tk = j / SPT, js = j % SPT;
-      const uint32_t f0 = tile_f0(tk);
-      if (f0 >= args.n) {               // wave-uniform exit (tiles ascend)
-        publish_records(args, nrec, lane);
-        wait_vmcnt<0>();                // no DMA may land after the workgroup ends
-        return;
-      }
-      if (js == 0 && tk > 0) dma_descs(tk + 1);   // tile k+1 behind tile k-1's last reads
-      const int sn = (s + R - 1) % R;   // slot of step j+R-1, freed by step j-1
-      ref[sn] = ref_of_step(j + R - 1);
-      issue(ref[sn], sn);
-      wait_vmcnt<(R - 1) * NCH>();      // step j's slot (and older DMAs) have landed
-
-      const FrameRef &r = ref[s];
-      const uint32_t sl = ring0 + s * SLOT;
-      const Header h = parse_header(sl + 16 * grp * LPF + r.rs);
-      uint4 v[NCH];
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) v[k] = lds_u128(sl + k * 1024 + 16 * lane);
-      bool do_sum;
-      const int32_t verdict = verdict_of(r, h, args.fwd_verdict, do_sum);
-      const int lo = r.rs + h.u, hi = r.rs + r.len;
-      const uint32_t wl = (lo & 1) ? 0x01000100u : 0x00010001u;
-      const uint32_t wh = wl << 8 | wl >> 24;
-      uint32_t acc_lo = 0, acc_hi = 0;
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) chunk_sum_fast(v[k], (k * LPF + gl) * 16, lo, hi, wl, wh, acc_lo, acc_hi);
-      const uint32_t P0 = group_sum_last<LPF>(acc_lo + (acc_hi << 8));
-      if (gl == LPF - 1 && r.exists)
-        lds_store_i32(rec + 4 * (js * G + grp),
-                      step_result(args, r, h, verdict, do_sum, P0, LPF * NCH, part + 4 * (js * G + grp)));
-      if (js == SPT - 1) {             // steps past n ran as no-ops
-        compiler_barrier();
-        finish_long_frames<LPF, NCH>(args, dsc0 + (tk & 1) * (kTile * 16), f0, rec, part, SPT, grp, gl);
-        nrec += flush_tile(args, rec, f0, lane);
-      }
-      ++j;
-    }
-  }
-}
-#endif  // XSKNF_AB
 
 // ---- phase 2: write-only pass of the parked checks (:108) and verdicts -------
 //
@@ -2399,9 +1847,6 @@ __device__ __forceinline__ T *uniform_ptr(T *p) {
   gT *const q = (gT *)uniform_u64(reinterpret_cast<uint64_t>(p));   // an integer made a global pointer ...
   return (T *)q;                                                     // ... then generic: inferable
 }
-#ifndef XSKNF_RES_FENCE   // A/B timing only: 0 drops the system-scope cache maintenance (unsafe)
-#define XSKNF_RES_FENCE 1
-#endif
 
 __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
   static_assert(kResBlockFrames == kWavesPerBlock * kResSpt * (kWave / kResLpf), "one round per block");
@@ -2479,7 +1924,7 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
         hdr[4] = b;
         if (hdr[3]) {
           // the host's writes of this batch (header, descriptors, frames), seen from this CU
-          if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
           // fwd and payload_mult in one 8-byte load (one round trip)
           const uint64_t fm = __hip_atomic_load(reinterpret_cast<uint64_t *>(&in[b].fwd), __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2520,7 +1965,7 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
       __syncthreads();   // the block's stores are done (workgroup release / acquire)
       if (threadIdx.x == 0) {
         if (hdr[3]) {
-          if (XSKNF_RES_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the checks and verdicts
           __hip_atomic_store(&r_out[b * kResGroup + g].done, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         last = wall_clock64();
@@ -2661,11 +2106,9 @@ int launch_lane(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel_lane launch");
 }
 
-template <int W, int LPF, int NCH, int U, bool TL, bool DMA, bool PFW = false, int SW = kWavesPerBlock>
+template <int W, int LPF, int NCH, int U, bool TL, int SW = kWavesPerBlock>
 int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  // the DMA stages / the window prefetch reuse the windows: every check deferred
-  if ((DMA || PFW) && a.defer_min_len != 0) return -EINVAL;
-  auto k = checksum_kernel_split<W, LPF, NCH, U, TL, DMA, PFW, SW>;
+  auto k = checksum_kernel_split<W, LPF, NCH, U, TL, SW>;
   if constexpr (SW > kWavesPerBlock) {
     // a block holding a whole CU's waves (and ~160 KiB of LDS) that the device
     // cannot make resident runs as the 4-wave shape with the static schedule
@@ -2675,10 +2118,10 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
       fits = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, SW * kWave, 0) == hipSuccess && b > 0;
       (void)hipGetLastError();
     }
-    if (!fits) return launch_split<W, LPF, NCH, U, TL, DMA, PFW, kWavesPerBlock>(a, stream, blocks_per_cu);
+    if (!fits) return launch_split<W, LPF, NCH, U, TL, kWavesPerBlock>(a, stream, blocks_per_cu);
   }
   uint32_t grid = grid_blocks(k, a.n, blocks_per_cu, kWave, SW);
-  constexpr uint32_t PT = patch_list_tiles<W, NCH, U, DMA, PFW, pooled_split(SW)>();
+  constexpr uint32_t PT = patch_list_tiles<W, NCH, U, pooled_split(SW)>();
   if constexpr (PT > 0) {
     // Enough blocks that every tile's check goes to a patch list, whatever
     // blocks_per_cu asks or the device's CU count (blocks past residency start
@@ -2699,28 +2142,13 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
   return finish_launch(a, stream, "checksum_kernel_split launch");
 }
 
-#ifdef XSKNF_AB
-template <int SW, bool NT, int MODE = 0>
-int launch_small(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  auto k = checksum_kernel_small<SW, NT, MODE>;
-  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kWave, SW)), dim3(SW * kWave), 0, stream, a);
-  return finish_launch(a, stream, "checksum_kernel_small launch");
-}
-#endif
 
 
-#ifdef XSKNF_AB
-template <int LPF, int NCH, int R>
-int launch_dma(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
-  auto k = checksum_kernel_dma<LPF, NCH, R>;
-  hipLaunchKernelGGL(k, dim3(grid_blocks(k, a.n, blocks_per_cu, kTile)), dim3(kBlock), 0, stream, a);
-  return finish_launch(a, stream, "checksum_kernel_dma launch");
-}
-#endif
 
 // Instantiated launch shapes: {lanes per frame, 16-B chunks per lane and pass,
 // frames per group and step (register) / items per group in flight (split),
-// LDS ring slots (0 = register kernel), kernel family, header window chunks}.
+// LDS ring slots (always 0: the LDS-DMA kernels were A/B material, removed in
+// round 5), kernel family, header window chunks}.
 struct Variant {
   int lpf, nch, u, ring;
   int (*fn)(const KernelArgs &, hipStream_t, int);
@@ -2737,19 +2165,12 @@ struct Variant {
 #define XSKNF_LA(N, S) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, 4, 2>, XSKNF_GPU_KERNEL_AUTO, 1024}
 // (A/B) lane kernel held to WPE waves per SIMD (window field 64 + 256 * WPE)
 #define XSKNF_LW(N, S, WPE) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, WPE>, XSKNF_GPU_KERNEL_AUTO, 64 + 256 * WPE}
-#define XSKNF_D(L, N, R) {L, N, 1, R, &launch_dma<L, N, R>}
 // split: window field = W, + 16 for the transposed (coalesced) window load
-#define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL, false>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
-// phase B through LDS-DMA (lds_ring field = 1); every check deferred (fused_stores mode 2)
-#define XSKNF_SD(W, L, N, U) {L, N, U, 1, &launch_split<W, L, N, U, true, true>, XSKNF_GPU_KERNEL_SPLIT, W + 16}
-// header windows prefetched by LDS-DMA one tile ahead (lds_ring field = 2); every check deferred
-#define XSKNF_SP(L, N, U) {L, N, U, 2, &launch_split<8, L, N, U, true, false, true>, XSKNF_GPU_KERNEL_SPLIT, 24}
+#define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
 // one 12-wave block per CU, its waves drawing the CU's tiles from a shared pool (window field + 32)
-#define XSKNF_SC(L, N, U) {L, N, U, 0, &launch_split<8, L, N, U, true, false, false, 12>, XSKNF_GPU_KERNEL_SPLIT, 56}
-// jumbo: one 8-wave block per CU (176 VGPRs: 2 waves per SIMD), W = 4
-#define XSKNF_SC4(L, N, U) {L, N, U, 0, &launch_split<4, L, N, U, true, false, false, 8>, XSKNF_GPU_KERNEL_SPLIT, 52}
-// (A/B) jumbo with one 12-wave block per CU (window field + 64)
-#define XSKNF_SC4W(L, N, U) {L, N, U, 0, &launch_split<4, L, N, U, true, false, false, 12>, XSKNF_GPU_KERNEL_SPLIT, 116}
+#define XSKNF_SC(L, N, U) {L, N, U, 0, &launch_split<8, L, N, U, true, 12>, XSKNF_GPU_KERNEL_SPLIT, 56}
+// jumbo: one 8-wave block per CU (174 VGPRs: 2 waves per SIMD), W = 4
+#define XSKNF_SC4(L, N, U) {L, N, U, 0, &launch_split<4, L, N, U, true, 8>, XSKNF_GPU_KERNEL_SPLIT, 52}
 const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
     XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_SC(16, 2, 2), XSKNF_S(8, 16, 3, 1, 1),
@@ -2766,11 +2187,7 @@ const Variant kVariants[] = {
     XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
     XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
     XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
-    XSKNF_SC4W(16, 3, 2), XSKNF_SC(16, 2, 3),
-#if XSKNF_BIG_STATIC
-    // the compact shape as one 16-wave block per CU, tiles dealt statically (window field 152)
-    {16, 2, 1, 0, &launch_split<8, 16, 2, 1, true, false, false, 16>, XSKNF_GPU_KERNEL_SPLIT, 152},
-#endif
+    XSKNF_SC(16, 2, 3),   // (jumbo in one 12-wave block per CU: 1520 vs 1456 us, r02 ab_pool_jumbo; removed r05)
     XSKNF_LP(5, 2),   // lane kernel with the tile pool: 64 B 59.65 vs 59.51 us, a tie (r02 ab_pool_lane.jsonl)
     // ... in 64-frame units (r05 ab_lane_pool / r05c): 64 B 58.8-59.1 vs 58.5-58.7 static (both write-through),
     // packed 64 B 37.3 vs 38.0-38.3, packed NIC 20.1-20.4 vs 22.4-22.7
@@ -2779,23 +2196,13 @@ const Variant kVariants[] = {
     // packed (-u) frames +1 us; per tile by the frames' spread: worst case +2 us (4 waves per SIMD forced)
     XSKNF_LT(5, 2), XSKNF_LT(4, 2), XSKNF_LT(5, 1), XSKNF_LA(5, 2), XSKNF_LA(5, 1),
     XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
-    XSKNF_SD(8, 16, 2, 2), XSKNF_SD(8, 16, 4, 1),   // LDS-DMA phase B: 1500 B 302 us vs 288 (r02 tune_dma)
-    XSKNF_SP(16, 2, 2), XSKNF_SP(16, 3, 1),         // window prefetch: +3-6 us on 1500 / IMIX / 570 (tune_pfw)
     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_L(4, 1),     XSKNF_L(4, 2),     XSKNF_L(5, 1),   // fewer VGPRs, more waves (r03 64 B A/B)
     XSKNF_LW(4, 1, 8), XSKNF_LW(4, 2, 6), XSKNF_LW(5, 2, 6), XSKNF_LW(5, 1, 8),
-    // small-frame kernel, 8 waves per SIMD (window field 128): 64 B 61.5-62.7 vs the lane kernel's 59.4-60.0 us
-    {1, 4, 1, 0, &launch_small<4, false>, XSKNF_GPU_KERNEL_AUTO, 128},
-    {1, 4, 1, 0, &launch_small<4, true>, XSKNF_GPU_KERNEL_AUTO, 160},   // nt window loads
-    {1, 4, 1, 0, &launch_small<4, false, 1>, XSKNF_GPU_KERNEL_AUTO, 192},   // timing only: no parse / sum
-    {1, 4, 1, 0, &launch_small<4, false, 2>, XSKNF_GPU_KERNEL_AUTO, 224},   // timing only: no LDS either
     XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
     XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
     XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
     XSKNF_V(64, 2, 8), XSKNF_V(64, 4, 4), XSKNF_V(64, 9, 2), XSKNF_V(64, 9, 4),
-    XSKNF_D(8, 1, 3),  XSKNF_D(8, 1, 4),  XSKNF_D(16, 1, 3), XSKNF_D(16, 2, 3), XSKNF_D(32, 2, 3),
-    XSKNF_D(32, 3, 2), XSKNF_D(32, 3, 3), XSKNF_D(64, 2, 3), XSKNF_D(64, 2, 4), XSKNF_D(64, 3, 3),
-    XSKNF_D(64, 4, 2), XSKNF_D(64, 4, 3),
 #endif
 };
 #undef XSKNF_V
@@ -2804,13 +2211,9 @@ const Variant kVariants[] = {
 #undef XSKNF_LT
 #undef XSKNF_LA
 #undef XSKNF_LW
-#undef XSKNF_D
 #undef XSKNF_S
-#undef XSKNF_SD
-#undef XSKNF_SP
 #undef XSKNF_SC
 #undef XSKNF_SC4
-#undef XSKNF_SC4W
 
 const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
   for (const Variant &v : kVariants) {
@@ -2820,7 +2223,7 @@ const Variant *find_variant(const xsknf_gpu_launch_cfg &c) {
           v.window == c.window_chunks && v.ring == c.lds_ring)
         return &v;
     } else if (v.lpf == c.lanes_per_frame && v.nch == c.chunks_per_lane && v.ring == c.lds_ring &&
-               (c.lds_ring || v.u == c.frames_per_group) && v.window == (c.window_chunks & ~31)) {
+               v.u == c.frames_per_group && v.window == (c.window_chunks & ~31)) {
       return &v;
     }
   }
