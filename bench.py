@@ -21,7 +21,10 @@ with its step fraction, kernel and committed PMC traffic): 64 B (config 2), a
 1M-frame IMIX batch (config 4's per-GPU shard), 9000 B jumbo frames in an
 unaligned UMEM (config 5), and config 4 -- the global 8,388,608-frame IMIX batch
 split into byte-balanced contiguous shards, one per rank (all of it on one GPU
-at N = 1, exactly config 4's 8-way split at N = 8).
+at N = 1, exactly config 4's 8-way split at N = 8); the NIC-checksummed variants
+(`*-nic`); and `64-13M`, config 2's frames as one 13M-frame batch (one
+lane-kernel launch instead of 13: what a 64 B step costs without its launch's
+ramp and drain).
 """
 from __future__ import annotations
 
@@ -60,6 +63,8 @@ WORKLOADS = {
     "570": (570, "aligned", 2048, "IMIX's middle size class alone: 570 B frames, aligned UMEM 2048 B chunks"),
     "imix": ("imix", "aligned", 2048, "IMIX 64/570/1500 B (7:4:1), 1M frames per GPU, aligned 2048 B chunks"),
     "jumbo": (9000, "unaligned", 0, "BASELINE config 5: 9000 B frames, unaligned-chunk UMEM, ~50% odd starts"),
+    "64-13M": (64, "aligned", 2048, "BASELINE config 2's frames (64 B, aligned UMEM 2048 B chunks) as ONE batch of "
+                                    "13 x the per-GPU frames: one lane-kernel launch, one ramp and drain for all of it"),
     "config4": ("imix", "aligned", 2048,
                 "BASELINE config 4: 8,388,608 IMIX 64/570/1500 B frames (7:4:1) split into byte-balanced "
                 "contiguous shards, one per GPU, aligned 2048 B chunks"),
@@ -86,7 +91,7 @@ def parse():
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU (config4: global frames "
                    f"= {CONFIG4_FRAMES} unless --config4-frames)")
     p.add_argument("--config4-frames", type=int, default=CONFIG4_FRAMES)
-    p.add_argument("--secondary", default="64,imix,jumbo,config4,1500-nic,imix-nic,64-nic,jumbo-nic",
+    p.add_argument("--secondary", default="64,imix,jumbo,config4,1500-nic,imix-nic,64-nic,jumbo-nic,64-13M",
                    help="comma list of extra workloads timed after the primary ('' = none)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=1)
@@ -211,7 +216,8 @@ def workload_lengths(name, args, world, rank):
         glens = frames.imix_lengths(args.config4_frames, np.random.default_rng(frames.SEED))
         lo, hi = shard_by_bytes(glens, world)[rank]
         return glens[lo:hi].astype(np.uint32), (lo, hi)
-    return frames._lens(args.frames, length, np.random.default_rng(frames.SEED + rank)), None
+    n = args.frames * (13 if name == "64-13M" else 1)
+    return frames._lens(n, length, np.random.default_rng(frames.SEED + rank)), None
 
 
 def rotation(lens: np.ndarray, args) -> int:

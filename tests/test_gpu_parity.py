@@ -235,6 +235,29 @@ def test_full_size_configs_bit_exact(dev, name, n, length, layout):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("n,layout", [((2 << 20) + 4097, "aligned"), ((17 << 20) + 5, "unaligned")],
+                         ids=["2M-aligned", "17M-packed"])
+def test_lane_kernel_large_batches(dev, n, layout):
+    """64 B frames: the lane kernel takes up to 16M frames in one launch (run()
+    in checksummer.hip), so a 2M-frame batch is one launch whose waves take
+    several times the tiles of a 1M-frame one, and a 17M-frame batch is a 16M
+    launch plus a short one; every verdict and byte equal to the oracle's (the
+    aligned batch through the write-through sector stores, the packed one
+    through the non-temporal ones)."""
+    umem, descs, lens = frames.device_batch(n, 64, layout=layout, device=dev, seed=79)
+    host = umem.cpu().numpy()
+    hd = descs.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1).copy()
+    frames.inject_edge_cases(frames.HostBatch(host, hd, layout), 0.01, seed=80)
+    umem.copy_(torch.from_numpy(host))
+    descs.copy_(torch.from_numpy(hd.view(np.int64).reshape(n, 2)))
+    v = Checksummer(frame_len_hint=64).process_batch(umem, descs)
+    gv, gu = _results(v, umem)
+    _, ov = O.c_time_batch(host, hd, threads=16, reps=1)
+    assert np.array_equal(gv, ov)
+    assert np.array_equal(gu, host)
+
+
+@pytest.mark.slow
 @pytest.mark.parametrize("length", [1500, "imix"])
 def test_batch_larger_than_one_launch(dev, length):
     """A batch of more than 1M frames runs as consecutive launches (run() in
