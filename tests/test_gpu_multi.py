@@ -24,6 +24,7 @@ import numpy as np
 import pytest
 
 from oracle import csum_oracle as O
+from tests import oracles
 from xsknf_amd import Checksummer, frames
 from xsknf_amd.shard import rebase_descs, shard_by_bytes, shard_spans
 
@@ -79,7 +80,7 @@ def test_config4_global_batch_in_byte_balanced_shards(dev):
         del local, ldt
     torch.cuda.synchronize()
     gu = umem.cpu().numpy()                                    # before the CPU oracle
-    _, ov = O.c_time_batch(host, hd, threads=16, reps=1)      # in place over the whole batch
+    _, ov = oracles.time_batch(host, hd)      # in place over the whole batch
     assert np.array_equal(gv, ov)
     assert np.array_equal(gu, host)
     assert (ov == -1).sum() > 0 and (ov == 0).sum() > 0.98 * n

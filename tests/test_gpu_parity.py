@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 from oracle import csum_oracle as O
+from tests import oracles
 from xsknf_amd import Checksummer, ChecksummerOptions, frames
 
 pytestmark = pytest.mark.gpu
@@ -219,7 +220,7 @@ def test_full_size_configs_bit_exact(dev, name, n, length, layout):
     hint, mean = int(lens.max()), int(lens.mean())
     v = Checksummer(frame_len_hint=hint, frame_len_mean=mean).process_batch(umem, descs)
     gv, gu = _results(v, umem)
-    _, ov = O.c_time_batch(host_in, host_descs, threads=16, reps=1)
+    _, ov = oracles.time_batch(host_in, host_descs)
     assert np.array_equal(gv, ov)
     assert np.array_equal(gu, host_in)
     # the clean frames are valid UDP frames: REDIRECT to iface 0
@@ -252,7 +253,7 @@ def test_lane_kernel_large_batches(dev, n, layout):
     descs.copy_(torch.from_numpy(hd.view(np.int64).reshape(n, 2)))
     v = Checksummer(frame_len_hint=64).process_batch(umem, descs)
     gv, gu = _results(v, umem)
-    _, ov = O.c_time_batch(host, hd, threads=16, reps=1)
+    _, ov = oracles.time_batch(host, hd)
     assert np.array_equal(gv, ov)
     assert np.array_equal(gu, host)
 
@@ -272,7 +273,7 @@ def test_batch_larger_than_one_launch(dev, length):
     descs.copy_(torch.from_numpy(hd.view(np.int64).reshape(n, 2)))
     v = Checksummer(frame_len_hint=int(lens.max())).process_batch(umem, descs)
     gv, gu = _results(v, umem)
-    _, ov = O.c_time_batch(host, hd, threads=16, reps=1)
+    _, ov = oracles.time_batch(host, hd)
     assert np.array_equal(gv, ov)
     assert np.array_equal(gu, host)
 
@@ -457,7 +458,7 @@ def test_full_size_nic_offloaded_bit_exact(dev, length, layout):
     before = host_in.copy()
     v = Checksummer(frame_len_hint=int(lens.max()), frame_len_mean=int(lens.mean())).process_batch(umem, descs)
     gv, gu = _results(v, umem)
-    _, ov = O.c_time_batch(host_in, hd, threads=16, reps=1)
+    _, ov = oracles.time_batch(host_in, hd)
     assert np.array_equal(gv, ov)
     assert np.array_equal(gu, host_in)
     offs = frames.HostBatch(before, hd, layout).frame_offsets().astype(np.int64)
@@ -935,7 +936,7 @@ def test_one_block_per_cu_asked_is_bit_exact(dev, shape):
         ctypes.c_void_p(umem.data_ptr()), umem.numel(), ctypes.c_void_p(descs.data_ptr()), n, 0,
         ctypes.byref(opts), ctypes.c_void_p(v.data_ptr()), ctypes.byref(cfg), None) == 0
     gv, gu = _results(v, umem)
-    _, ov = O.c_time_batch(host, hd, threads=16, reps=1)
+    _, ov = oracles.time_batch(host, hd)
     assert np.array_equal(gv, ov)
     assert np.array_equal(gu, host)
 

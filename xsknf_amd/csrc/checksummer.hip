@@ -818,7 +818,9 @@ __device__ __forceinline__ void store_sector16(uint8_t *p, uint4 v, bool wt XSKN
   if (!guard_ok(p, 16, site)) return;
 #endif
   const u32x4 x = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(x) : "memory");
+  // (s_nop 1: the store reads its data registers after issue, and the next
+  // instruction hipcc places after the statement may overwrite them)
+  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
 }
 
 // The wave's patched sectors, 16 per instruction: lanes 4i..4i+3 write the 4
