@@ -83,3 +83,36 @@ def test_check_fingerprint_of_shards_adds_up_to_the_whole(world):
         umem[a], umem[c] = umem[c].clone(), umem[a].clone()
         umem[a + 1], umem[c + 1] = umem[c + 1].clone(), umem[a + 1].clone()
     assert bench.check_fingerprint(umem, whole_d, 0) != whole
+
+
+def test_cpu_baseline_windows_and_pinning():
+    """cpu_baseline (kind "reference" where oracle/_ref is built, else the
+    restatement) times three windows, reports their median with min / max, and
+    pins one thread to the LAST CPU of the affinity mask, several threads to its
+    last CPUs."""
+    import os
+    from xsknf_amd import frames
+    b = frames.aligned_batch(2048, 1500, seed=61)
+    res = {"sample": (b.umem.copy(), b.descs, b.n)}
+    mask = sorted(os.sched_getaffinity(0))
+    for threads in (1, min(2, len(mask))):
+        c = bench.cpu_baseline(res, 0.3, threads, check=False)
+        sp = c["spread"]
+        assert sp["windows"] == 3 and sp["min"] <= c["value"] <= sp["max"]
+        assert c["cores"] == threads and c["unit"] == "GB/s checksummed"
+        assert c["pinned_to"] == bench._cpu_list(mask[-threads:])
+        assert c["kind"] in ("reference", "port")
+        assert c["mpps"] > 0
+
+
+def test_cpu_list_ranges():
+    assert bench._cpu_list([0, 1, 2, 3, 7, 9, 10]) == "0-3,7,9-10"
+    assert bench._cpu_list([5]) == "5"
+
+
+def test_lane_batch_workload_is_thirteen_batches():
+    class A:
+        frames = 1024
+        config4_frames = 8192
+    lens, span = bench.workload_lengths("64-13M", A, 1, 0)
+    assert lens.shape[0] == 13 * 1024 and span is None and int(lens.max()) == 64
