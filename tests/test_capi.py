@@ -118,6 +118,7 @@ def test_launch_shape_for_lengths_without_gpu():
     assert shape(1500, 352)[3] == 24 and shape(1500, 511)[3] == 24 and shape(4000, 1024)[3] == 56
     assert shape(9000, 9000)[3] == 52          # jumbo: 4-chunk window, tile pool, whatever the mean
     assert shape(64, 64)[1] == 1               # lane kernel
+    assert shape(64, 64)[3] == 1024            # windows transposed where a tile's frames lie apart
     assert lib.xsknf_gpu_launch_cfg_for_lens(1500, 1500, None) == -errno.EINVAL
 
 

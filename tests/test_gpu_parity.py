@@ -293,6 +293,9 @@ PRODUCT_SHAPES = [
     (16, 3, 2, 0, 0, 1, 52), (16, 3, 2, 0, 1, 1, 52), (16, 3, 2, 0, 2, 1, 52), (16, 3, 2, 0, 18, 1, 52),
     # the lane kernel (short frames) under every store mode
     (1, 5, 2, 0, 1), (1, 5, 2, 0, 9), (1, 5, 2, 0, 5), (1, 5, 2, 0, 2), (1, 5, 2, 0, 0),
+    # ... and its default since round 5: windows transposed where a tile's frames lie apart (window field 1024)
+    (1, 5, 2, 0, 1, 0, 1024), (1, 5, 2, 0, 9, 0, 1024), (1, 5, 2, 0, 5, 0, 1024), (1, 5, 2, 0, 2, 0, 1024),
+    (1, 5, 2, 0, 0, 0, 1024),
     # the zero-copy host path's small-batch group shapes
     (32, 3, 2, 0, 0), (32, 3, 2, 0, 1), (32, 3, 2, 0, 5), (64, 2, 4, 0, 2), (64, 2, 4, 0, 1),
 ]

@@ -2177,8 +2177,9 @@ const Variant kVariants[] = {
     // the product's shapes: default_cfg()'s split kernels, one per size class ...
     XSKNF_S(4, 16, 2, 2, 1), XSKNF_S(8, 16, 2, 2, 1), XSKNF_SC(16, 2, 2), XSKNF_S(8, 16, 3, 1, 1),
     XSKNF_S(4, 16, 3, 2, 1), XSKNF_SC4(16, 3, 2),
-    // ... the lane kernel for short frames ...
-    XSKNF_L(5, 2),
+    // ... the lane kernel for short frames: windows loaded transposed where a
+    // tile's frames lie apart (the default since round 5), and per lane ...
+    XSKNF_LA(5, 2), XSKNF_L(5, 2),
     // ... and the zero-copy host path's small-batch group shapes (host_path.hip)
     XSKNF_V(32, 3, 2), XSKNF_V(64, 2, 4),
 #ifdef XSKNF_AB
@@ -2195,8 +2196,10 @@ const Variant kVariants[] = {
     // packed 64 B 37.3 vs 38.0-38.3, packed NIC 20.1-20.4 vs 22.4-22.7
     XSKNF_LP(5, 1),
     // transposed window loads (r04 ab_lane_transposed*.jsonl): aligned 64 B NIC -1 us, worst case +0.3,
-    // packed (-u) frames +1 us; per tile by the frames' spread: worst case +2 us (4 waves per SIMD forced)
-    XSKNF_LT(5, 2), XSKNF_LT(4, 2), XSKNF_LT(5, 1), XSKNF_LA(5, 2), XSKNF_LA(5, 1),
+    // packed (-u) frames +1 us; per tile by the frames' spread: worst case +2 us (4 waves per SIMD forced);
+    // round 5, with the write-through sectors (ab_matrix_r05l): all transposed 57.1-57.7 vs 58.2-58.8 us,
+    // packed NIC +1 us; per tile (XSKNF_LA(5, 2)) 56.7-57.1: the product's since
+    XSKNF_LT(5, 2), XSKNF_LT(4, 2), XSKNF_LT(5, 1), XSKNF_LA(5, 1),
     XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_L(4, 1),     XSKNF_L(4, 2),     XSKNF_L(5, 1),   // fewer VGPRs, more waves (r03 64 B A/B)
@@ -2252,7 +2255,9 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   // Infinity Cache from its previous pass -- bench.py's rotation):
   //  * hint <= 128: the lane kernel (one lane per frame, 5-chunk window), every
   //    check in-line as its whole 64-byte sector, non-temporal: 64 B 57.6 us
-  //    [split kernel 60.3-61.3];
+  //    [split kernel 60.3-61.3]; round 5: written through where a tile's frames
+  //    lie apart, and there the windows loaded transposed (one request per
+  //    frame): 56.7-57.1 vs 58.2-58.8 (profiles/r05/ab/ab_matrix_r05l.jsonl);
   //  * <= 4 KiB: the split kernel, 8-chunk window (the frame's whole first
   //    128-byte line, so phase B never refetches it), 16 x 2 items, two in
   //    flight, every check deferred and patched once the stream is done
@@ -2273,7 +2278,8 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   c.lanes_per_frame = 16;
   if (hint <= 128) {
     c.kernel = XSKNF_GPU_KERNEL_AUTO;
-    c.lanes_per_frame = 1; c.window_chunks = 0; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
+    // (+ 1024: windows loaded transposed where a tile's frames lie apart)
+    c.lanes_per_frame = 1; c.window_chunks = 1024; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
   } else if (hint + 15 <= 4096) {
     // the CU-wide tile pool (+ 32) but for a known mix of mostly short frames
     // (IMIX: 115.9 vs 114.3 us with 4-wave blocks and the static schedule)
@@ -2315,6 +2321,7 @@ int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_de
 
 constexpr uint32_t kLaunchFrames = 1u << 20;
 constexpr uint32_t kLaneLaunchFrames = 1u << 24;
+constexpr uint32_t kLaneTransposedMaxFrames = 2u << 20;
 
 int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
@@ -2347,13 +2354,25 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   // 50.2 us per 1M frames in one launch against 58.6 in 13 launches, 4M 55.4
   // against 57.9 (profiles/r05/ab/ab_lane_launch_frames.jsonl).
   const uint32_t lf = v->lpf == 1 && v->kernel != XSKNF_GPU_KERNEL_SPLIT ? kLaneLaunchFrames : kLaunchFrames;
+  // The lane kernel's per-tile transposed windows (window field 1024) pay off
+  // in a launch of up to a few M frames, per-lane loads in a longer one (64 B,
+  // profiles/r05/ab/ab_lane_la_r05n.jsonl: 1M frames 57.5-57.7 vs 58.3-59.0 us,
+  // 13M frames in one launch 701-710 vs 655-662 us): a longer launch runs as
+  // the per-lane shape.
+  const Variant *longer = v;
+  if (v->kernel == XSKNF_GPU_KERNEL_AUTO && v->lpf == 1 && v->window == 1024) {
+    xsknf_gpu_launch_cfg c = cfg;
+    c.window_chunks = 0;
+    if (const Variant *w = find_variant(c)) longer = w;
+  }
   for (uint32_t off = 0; off < base.n; off += lf) {
     KernelArgs p = a;
     p.descs = base.descs + off;
     p.verdicts = base.verdicts + off;
     p.n = base.n - off < lf ? base.n - off : lf;
     p.seq = seq.fetch_add(1, std::memory_order_relaxed);
-    const int rc = v->fn(p, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
+    const Variant *lv = p.n > kLaneTransposedMaxFrames ? longer : v;
+    const int rc = lv->fn(p, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
     if (rc) return rc;
   }
   return 0;
