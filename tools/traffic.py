@@ -102,7 +102,10 @@ def main():
     bench = json.load(open(os.path.join(d, "FETCH_SIZE.bench.json")))
     kalone = bench["roofline"].get("summing_kernel_alone")
     # launches per step: a batch of more than 1M frames runs as 1M-frame launches (config 4 on one GPU)
-    per_step = -(-int(bench["config"]["frames_per_gpu"]) // (1 << 20))
+    # (the lane kernel, frames <= 128 B, takes up to 16M frames per launch)
+    per_step = -(-int(bench["config"]["frames_per_gpu"]) // (1 << (24 if int(bench["config"].get("frame_len") or 0) == 64 and
+                                                                       "lane" in bench["roofline"].get("kernels", "")
+                                                                       else 20)))
     tail = per_step * (3 + int(bench.get("kernel_steps", 50))) if kalone else 0
     fetch = dispatches(d, "FETCH_SIZE")
     write = dispatches(d, "WRITE_SIZE")
