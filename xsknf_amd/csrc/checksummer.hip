@@ -2165,6 +2165,8 @@ struct Variant {
 #define XSKNF_LT(N, S) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, 1, 1>, XSKNF_GPU_KERNEL_AUTO, 512}
 // ... transposed per tile where the tile's frames lie apart (window field 1024)
 #define XSKNF_LA(N, S) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, 4, 2>, XSKNF_GPU_KERNEL_AUTO, 1024}
+// (A/B) the pooled lane kernel with the per-tile transposed windows (window field 1056)
+#define XSKNF_LPA(N, S) {1, N, S, 0, &launch_lane<N, S, 16, 4, 2>, XSKNF_GPU_KERNEL_AUTO, 1056}
 // (A/B) lane kernel held to WPE waves per SIMD (window field 64 + 256 * WPE)
 #define XSKNF_LW(N, S, WPE) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, WPE>, XSKNF_GPU_KERNEL_AUTO, 64 + 256 * WPE}
 // split: window field = W, + 16 for the transposed (coalesced) window load
@@ -2195,6 +2197,7 @@ const Variant kVariants[] = {
     // ... in 64-frame units (r05 ab_lane_pool / r05c): 64 B 58.8-59.1 vs 58.5-58.7 static (both write-through),
     // packed 64 B 37.3 vs 38.0-38.3, packed NIC 20.1-20.4 vs 22.4-22.7
     XSKNF_LP(5, 1),
+    XSKNF_LPA(5, 1), XSKNF_LPA(5, 2),
     // transposed window loads (r04 ab_lane_transposed*.jsonl): aligned 64 B NIC -1 us, worst case +0.3,
     // packed (-u) frames +1 us; per tile by the frames' spread: worst case +2 us (4 waves per SIMD forced);
     // round 5, with the write-through sectors (ab_matrix_r05l): all transposed 57.1-57.7 vs 58.2-58.8 us,
@@ -2216,6 +2219,7 @@ const Variant kVariants[] = {
 #undef XSKNF_LT
 #undef XSKNF_LA
 #undef XSKNF_LW
+#undef XSKNF_LPA
 #undef XSKNF_S
 #undef XSKNF_SC
 #undef XSKNF_SC4
