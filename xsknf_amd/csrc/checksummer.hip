@@ -2203,6 +2203,7 @@ const Variant kVariants[] = {
     // round 5, with the write-through sectors (ab_matrix_r05l): all transposed 57.1-57.7 vs 58.2-58.8 us,
     // packed NIC +1 us; per tile (XSKNF_LA(5, 2)) 56.7-57.1: the product's since
     XSKNF_LT(5, 2), XSKNF_LT(4, 2), XSKNF_LT(5, 1), XSKNF_LA(5, 1),
+    XSKNF_LA(5, 4), XSKNF_LA(4, 2),   // (r05y: 62.8-63.1 and 57.3-57.9 vs 57.0-57.6 us)
     XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
     XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
     XSKNF_L(4, 1),     XSKNF_L(4, 2),     XSKNF_L(5, 1),   // fewer VGPRs, more waves (r03 64 B A/B)
