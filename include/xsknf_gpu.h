@@ -77,7 +77,12 @@ XSKNF_GPU_API int xsknf_gpu_device_count(int *count);
  *
  * Descriptors whose [addr, addr+len) lies outside [0, umem_size) are not
  * touched and get verdict -1 (the kernel's own rx validation guarantees the
- * reference never sees one).
+ * reference never sees one).  The frames of a batch are distinct UMEM chunks,
+ * as an rx ring's are (the reference's serial loop would make two descriptors
+ * of the same bytes order-dependent; here their frames are checksummed
+ * concurrently).
+ * A batch runs as one launch per 1M frames (per 16M for frames of at most
+ * 128 bytes, where one launch over more frames measured faster).
  * Returns 0, -EINVAL on bad arguments, -EIO on a HIP launch error.
  */
 XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
