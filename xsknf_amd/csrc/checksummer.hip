@@ -2283,8 +2283,11 @@ void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean) {
   c.lanes_per_frame = 16;
   if (hint <= 128) {
     c.kernel = XSKNF_GPU_KERNEL_AUTO;
-    // (+ 1024: windows loaded transposed where a tile's frames lie apart)
+    // (+ 1024: windows loaded transposed where a tile's frames lie apart; 3
+    // blocks per CU of the 4 that fit: 64 B 56.7-57.1 vs 56.8-57.2 us, packed
+    // 64 B NIC 20.2-20.3 vs 22.5-22.8, nothing slower -- ab_lane_bpc_r05z.jsonl)
     c.lanes_per_frame = 1; c.window_chunks = 1024; c.chunks_per_lane = 5; c.frames_per_group = 2; c.fused_stores = 1;
+    c.blocks_per_cu = 3;
   } else if (hint + 15 <= 4096) {
     // the CU-wide tile pool (+ 32) but for a known mix of mostly short frames
     // (IMIX: 115.9 vs 114.3 us with 4-wave blocks and the static schedule)
@@ -2377,7 +2380,11 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
     p.n = base.n - off < lf ? base.n - off : lf;
     p.seq = seq.fetch_add(1, std::memory_order_relaxed);
     const Variant *lv = p.n > kLaneTransposedMaxFrames ? longer : v;
-    const int rc = lv->fn(p, static_cast<hipStream_t>(stream), cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
+    // (and a longer launch as many blocks per CU as fit: 13M frames 660 us at
+    // 4 per CU against 695-699 at the 3 of the default lane shape,
+    // profiles/r05/ab/ab_lane_bpc_r05z*.jsonl)
+    const int bpc = lv != v ? 8 : (cfg.blocks_per_cu ? cfg.blocks_per_cu : 8);
+    const int rc = lv->fn(p, static_cast<hipStream_t>(stream), bpc);
     if (rc) return rc;
   }
   return 0;
