@@ -44,7 +44,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="1500")
     ap.add_argument("--variants", default="")
-    ap.add_argument("--bpc", default="8")
+    ap.add_argument("--bpc", default="0",
+                    help="blocks per CU to try (comma list); 0 = the product's own choice for the default shape "
+                         "(default_cfg), 8 (as many as fit) for the others")
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=10)
@@ -78,7 +80,7 @@ def main():
         if s not in shapes:
             shapes.append(s)
     bpcs = [int(x) for x in a.bpc.split(",")]
-    cfgs = [(s, b) for s in shapes for b in bpcs]
+    cfgs = [(s, b if b else (dflt.blocks_per_cu if i == 0 else 8)) for i, s in enumerate(shapes) for b in bpcs]
     stream = torch.cuda.current_stream()
     umem = umem0.clone()
     verd = torch.empty(n, dtype=torch.int32, device=dev)
