@@ -971,6 +971,27 @@ def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
     assert max(tiles) <= limit, tiles
 
 
+@pytest.mark.parametrize("length,n", [(9000, 4 * 120 * 64), (9000, 4 * 104 * 64 + 1), ("imix", 4 * 72 * 64 + 4095)],
+                         ids=["jumbo-120", "jumbo-104", "imix"])
+def test_grid_sizing_on_a_smaller_device(length, n):
+    """launch_split's grid on a device of 4 CUs (XSKNF_GPU_CU_LIMIT, a test hook
+    read once per process, hence the child): a pool block of bt tiles has
+    bt + (parts - 1) * SW units, so a jumbo block (quarters, 8 waves of 16-unit
+    lists) holds 104 tiles, not SW * (PT - 1) = 120 -- at 4 x 120 tiles the grid
+    must be 5 blocks, and every frame still bit-exact."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, XSKNF_GPU_CU_LIMIT="4")
+    out = subprocess.run([sys.executable, os.path.join(root, "tests", "cu_limit_child.py"), "--frames", str(n),
+                          "--length", str(length), "--layout", "unaligned" if length == 9000 else "aligned"],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["cus_limit"] == "4"
+    assert r["bad_verdicts"] == 0 and r["bad_bytes"] == 0, r
+
+
 @pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 18, 1, 52), (16, 3, 2, 0, 0, 1, 52),
                                    pytest.param((1, 5, 2, 0, 1, 0, 32),
                                                 marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only")),

@@ -1163,6 +1163,12 @@ constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with 
 // window slots, 4-tile lists -- and its 16-wave static twin tied the default
 // and were removed in round 5: DESIGN 7.)
 constexpr bool pooled_split(int sw) { return sw > kWavesPerBlock; }
+// The parts each of a pool block's last SW tiles runs as: halves up to 4 KiB,
+// quarters for jumbo (W = 4).  XSKNF_JUMBO_PARTS (A/B): another count for jumbo.
+#ifndef XSKNF_JUMBO_PARTS
+#define XSKNF_JUMBO_PARTS 4
+#endif
+constexpr uint32_t pool_parts(int w) { return w == 4 ? XSKNF_JUMBO_PARTS : 2u; }
 
 // The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
 // a 16-unit list (64 KiB of its block's 135 KiB): with every check deferred
@@ -1328,7 +1334,7 @@ void checksum_kernel_split(const KernelArgs args) {
   // profiles/r02/ab_pool.jsonl), quarters for jumbo tiles (W = 4), which
   // stream for ~160 us each.  (Whole tiles only: IMIX level, 1500 B +6-7 us;
   // profiles/r04/ab/ab_pool_no_halves*.)
-  constexpr uint32_t kParts = W == 4 ? 4u : 2u;
+  constexpr uint32_t kParts = pool_parts(W);
   const uint32_t nsplit = kPool ? min(bt, static_cast<uint32_t>(SW)) : 0u;
   const uint32_t nfull = bt - nsplit;
   const uint32_t units = nfull + kParts * nsplit;
@@ -2020,6 +2026,13 @@ int device_cus() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       return 256;
+    // XSKNF_GPU_CU_LIMIT (test hook): size the grids as on a device with that
+    // many CUs (a compute partition has 32), so the grid-sizing bounds for
+    // smaller devices are exercised on this one (tests/test_gpu_parity.py)
+    if (const char *lim = getenv("XSKNF_GPU_CU_LIMIT")) {
+      const int l = atoi(lim);
+      if (l > 0 && l < cus) cus = l;
+    }
     cache[dev] = cus;
   }
   return cache[dev];
@@ -2135,7 +2148,11 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
     // not these kernels -- DESIGN 3; tested by test_no_wave_passes_its_patch_list.)
     if (a.tail_scatter) {
       const uint32_t tiles = (a.n + kWave - 1) / kWave;
-      constexpr uint32_t per_block = pooled_split(SW) ? SW * (PT - 1) : SW * PT;
+      // (a pool block of bt >= SW tiles has bt + (parts - 1) * SW units, and its
+      // waves' lists hold SW * PT: so at most SW * (PT - parts + 1) tiles -- the
+      // jumbo shape's 16-unit lists with quarters hold 104 tiles, not the 120 of
+      // SW * (PT - 1), which only a device of fewer than ~160 CUs reaches)
+      constexpr uint32_t per_block = pooled_split(SW) ? SW * (PT - pool_parts(W) + 1) : SW * PT;
       const uint32_t fit = (tiles + per_block - 1) / per_block;
       if (grid < fit) grid = fit;
     }
