@@ -989,6 +989,7 @@ def test_grid_sizing_on_a_smaller_device(length, n):
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["cus_limit"] == "4"
+    assert r["window_chunks"] == (52 if length == 9000 else 56)   # jumbo / 1500 B pooled shapes
     assert r["bad_verdicts"] == 0 and r["bad_bytes"] == 0, r
 
 
