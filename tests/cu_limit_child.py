@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--frames", type=int, required=True)
     ap.add_argument("--length", default="9000")
     ap.add_argument("--layout", default="unaligned")
+    ap.add_argument("--mean", action="store_true", help="pass the batch's mean length too (static IMIX shape)")
     a = ap.parse_args()
     length = int(a.length) if a.length.isdigit() else a.length
     dev = torch.device("cuda:0")
@@ -39,7 +40,8 @@ def main():
     descs.copy_(torch.from_numpy(hd.view(np.int64).reshape(n, 2)))
     # the batch's longest frame as the hint: the shape the product picks for it
     # (jumbo: the 8-wave pooled blocks with quarters)
-    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=int(lens.max()))
+    cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=int(lens.max()),
+                     frame_len_mean=int(lens.mean()) if a.mean else 0)
     v = cs.process_batch(umem, descs)
     torch.cuda.synchronize()
     gv, gu = v.cpu().numpy(), umem.cpu().numpy()

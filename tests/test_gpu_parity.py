@@ -971,25 +971,29 @@ def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
     assert max(tiles) <= limit, tiles
 
 
-@pytest.mark.parametrize("length,n", [(9000, 4 * 120 * 64), (9000, 4 * 104 * 64 + 1), ("imix", 4 * 72 * 64 + 4095)],
-                         ids=["jumbo-120", "jumbo-104", "imix"])
-def test_grid_sizing_on_a_smaller_device(length, n):
+@pytest.mark.parametrize("length,n,window", [(9000, 4 * 120 * 64, 52), (9000, 4 * 104 * 64 + 1, 52),
+                                             ("imix", 4 * 72 * 64 + 4095, 56), ("imix-mean", 4 * 8 * 24 * 64 + 4095, 24),
+                                             (64, 300_000, 1024)],
+                         ids=["jumbo-120", "jumbo-104", "imix-pool", "imix-static", "64-lane"])
+def test_grid_sizing_on_a_smaller_device(length, n, window):
     """launch_split's grid on a device of 4 CUs (XSKNF_GPU_CU_LIMIT, a test hook
     read once per process, hence the child): a pool block of bt tiles has
     bt + (parts - 1) * SW units, so a jumbo block (quarters, 8 waves of 16-unit
     lists) holds 104 tiles, not SW * (PT - 1) = 120 -- at 4 x 120 tiles the grid
-    must be 5 blocks, and every frame still bit-exact."""
+    must be 5 blocks, and every frame still bit-exact.  The pooled
+    W = 8, static and lane shapes at (or past) their bounds at 4 CUs too."""
     import json
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, XSKNF_GPU_CU_LIMIT="4")
-    out = subprocess.run([sys.executable, os.path.join(root, "tests", "cu_limit_child.py"), "--frames", str(n),
-                          "--length", str(length), "--layout", "unaligned" if length == 9000 else "aligned"],
+    args = ["--frames", str(n), "--length", str(length).replace("-mean", ""),
+            "--layout", "unaligned" if length == 9000 else "aligned"] + (["--mean"] if length == "imix-mean" else [])
+    out = subprocess.run([sys.executable, os.path.join(root, "tests", "cu_limit_child.py")] + args,
                          capture_output=True, text=True, timeout=240, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["cus_limit"] == "4"
-    assert r["window_chunks"] == (52 if length == 9000 else 56)   # jumbo / 1500 B pooled shapes
+    assert r["window_chunks"] == window   # the shape the product picks: jumbo / W = 8 pooled, static, lane
     assert r["bad_verdicts"] == 0 and r["bad_bytes"] == 0, r
 
 
