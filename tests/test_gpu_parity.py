@@ -944,6 +944,52 @@ def test_one_block_per_cu_asked_is_bit_exact(dev, shape):
     assert np.array_equal(gu, host)
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("length,n,mean,window", [(64, 20000, False, 1024), (1500, 20000, False, 56),
+                                                  ("imix", 20000, True, 24), ("imix", 20000, False, 56),
+                                                  (9000, 6000, False, 52)],
+                         ids=["64-lane", "1500-pool", "imix-static", "imix-pool", "jumbo-pool"])
+def test_umem_past_the_patch_list_index(dev, length, n, mean, window):
+    """A UMEM of 128 GiB or more (kPatchMaxUmem: the patch lists index 64-byte
+    sectors in 32 bits) parks its checks for scatter_checks instead of the lists
+    (DESIGN 3).  A 128 GiB + 64 MiB device UMEM (MI355X holds 288 GB) with the
+    batch's frames placed past 128 GiB, every product shape: every verdict and
+    byte matches the oracle."""
+    big_size = (1 << 37) + (64 << 20)
+    free, _ = torch.cuda.mem_get_info(dev)
+    if free < big_size + (8 << 30):
+        pytest.skip(f"{free >> 30} GiB free on the device")
+    if length == 9000:
+        b = frames.unaligned_batch(n, length, seed=n)
+    else:
+        b = frames.aligned_batch(n, length, seed=n)
+    frames.inject_edge_cases(b, 0.02, seed=n + 1)
+    lens = b.descs["len"]
+    ou, ov = run_oracle(b)
+    size = b.umem.size
+    base_off = (big_size - size) & ~4095
+    assert base_off >= 1 << 37
+    big = torch.empty(big_size, dtype=torch.uint8, device=dev)
+    try:
+        big[base_off:base_off + size].copy_(torch.from_numpy(b.umem))
+        d = b.descs.copy()
+        mask = np.uint64((1 << frames.OFFSET_SHIFT) - 1)
+        d["addr"] = ((d["addr"] & mask) + np.uint64(base_off)) | (d["addr"] & ~mask)
+        descs = torch.from_numpy(d.view(np.uint8).reshape(-1, 16).copy()).to(dev)
+        cs = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=int(lens.max()),
+                         frame_len_mean=int(lens.mean()) if mean else 0)
+        assert cs.launch_cfg().window_chunks == window
+        v = cs.process_batch(big, descs)
+        gv, gu = _results(v, big[base_off:base_off + size])
+    finally:
+        del big
+        torch.cuda.empty_cache()
+    assert np.array_equal(gv, ov)
+    if not np.array_equal(gu, ou):
+        diff = np.nonzero(gu != ou)[0]
+        raise AssertionError(f"{diff.size} UMEM bytes differ, first at {diff[:10]}")
+
+
 TL_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "tl", "libxsknf_gpu.so")
 
 
