@@ -1164,11 +1164,9 @@ constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with 
 // and were removed in round 5: DESIGN 7.)
 constexpr bool pooled_split(int sw) { return sw > kWavesPerBlock; }
 // The parts each of a pool block's last SW tiles runs as: halves up to 4 KiB,
-// quarters for jumbo (W = 4).  XSKNF_JUMBO_PARTS (A/B): another count for jumbo.
-#ifndef XSKNF_JUMBO_PARTS
-#define XSKNF_JUMBO_PARTS 4
-#endif
-constexpr uint32_t pool_parts(int w) { return w == 4 ? XSKNF_JUMBO_PARTS : 2u; }
+// quarters for jumbo (W = 4; halves 1469.5-1470.7, eighths 1471.1-1471.5 vs
+// 1459.2-1461.0 us, NIC +10..14 us -- profiles/r05/ab/ab_jumbo_parts_r05jp.jsonl).
+constexpr uint32_t pool_parts(int w) { return w == 4 ? 4u : 2u; }
 
 // The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
 // a 16-unit list (64 KiB of its block's 135 KiB): with every check deferred
