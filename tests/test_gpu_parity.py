@@ -1024,10 +1024,12 @@ def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
 def test_grid_sizing_on_a_smaller_device(length, n, window):
     """launch_split's grid on a device of 4 CUs (XSKNF_GPU_CU_LIMIT, a test hook
     read once per process, hence the child): a pool block of bt tiles has
-    bt + (parts - 1) * SW units, so a jumbo block (quarters, 8 waves of 16-unit
-    lists) holds 104 tiles, not SW * (PT - 1) = 120 -- at 4 x 120 tiles the grid
-    must be 5 blocks, and every frame still bit-exact.  The pooled
-    W = 8, static and lane shapes at (or past) their bounds at 4 CUs too."""
+    bt + (parts - 1) * k * SW units, so a jumbo block (its last 2 SW tiles in
+    quarters, 8 waves of 16-unit lists) holds 80 tiles, not SW * (PT - 1) = 120
+    (round 4's bound; 104 with the last SW tiles split) -- at 4 x 120 and
+    4 x 104 tiles the grid must grow past 4 blocks, and every frame still
+    bit-exact.  The pooled W = 8, static and lane shapes at (or past)
+    their bounds at 4 CUs too."""
     import json
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

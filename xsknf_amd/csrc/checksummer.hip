@@ -1163,10 +1163,15 @@ constexpr uint64_t kPatchMaxUmem = 1ull << 37;   // sector index: 32 bits (with 
 // window slots, 4-tile lists -- and its 16-wave static twin tied the default
 // and were removed in round 5: DESIGN 7.)
 constexpr bool pooled_split(int sw) { return sw > kWavesPerBlock; }
-// The parts each of a pool block's last SW tiles runs as: halves up to 4 KiB,
+// The parts each of a pool block's last tiles runs as: halves up to 4 KiB,
 // quarters for jumbo (W = 4; halves 1469.5-1470.7, eighths 1471.1-1471.5 vs
-// 1459.2-1461.0 us, NIC +10..14 us -- profiles/r05/ab/ab_jumbo_parts_r05jp.jsonl).
+// 1459.2-1461.0 us, NIC +10..14 us -- profiles/r05/ab/ab_jumbo_parts_r05jp.jsonl),
+// and how many: the last SW tiles, the last 2 SW for jumbo (1445.2-1445.7 vs
+// 1447.9-1448.8 us and 1455.4-1456.3 vs 1456.4-1459.2 on a second box, every
+// interleaved round faster, NIC -1..-2 us; as many as the lists hold, leaving
+// the waves no slack to balance: +50 us -- ab_jumbo_split_tiles_r05jk.jsonl).
 constexpr uint32_t pool_parts(int w) { return w == 4 ? 4u : 2u; }
+constexpr uint32_t pool_split_k(int w) { return w == 4 ? 2u : 1u; }
 
 // The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
 // a 16-unit list (64 KiB of its block's 135 KiB): with every check deferred
@@ -1326,14 +1331,14 @@ void checksum_kernel_split(const KernelArgs args) {
   const uint32_t nb = gridDim.x;
   const uint32_t bt = ntiles > blockIdx.x ? (ntiles - blockIdx.x + nb - 1) / nb : 0u;   // the block's tiles
   const auto tile_of = [&](uint32_t k) { return blockIdx.x + k * nb; };
-  // The pool's units: the block's tiles, except that its last SW tiles run as
-  // kParts parts each, so the waves' streams end closer together: halves up to
+  // The pool's units: the block's tiles, except that its last SW tiles (2 SW
+  // for jumbo) run as kParts parts each, so the waves' streams end closer together: halves up to
   // 4 KiB (quarters there: 570 B 165 vs 151 us, 1024 B 213 vs 205 --
   // profiles/r02/ab_pool.jsonl), quarters for jumbo tiles (W = 4), which
   // stream for ~160 us each.  (Whole tiles only: IMIX level, 1500 B +6-7 us;
   // profiles/r04/ab/ab_pool_no_halves*.)
   constexpr uint32_t kParts = pool_parts(W);
-  const uint32_t nsplit = kPool ? min(bt, static_cast<uint32_t>(SW)) : 0u;
+  const uint32_t nsplit = kPool ? min(bt, pool_split_k(W) * static_cast<uint32_t>(SW)) : 0u;
   const uint32_t nfull = bt - nsplit;
   const uint32_t units = nfull + kParts * nsplit;
   const auto pool_unit = [&](uint32_t p) { return p < units ? p : kNoTile; };
@@ -2146,11 +2151,12 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
     // not these kernels -- DESIGN 3; tested by test_no_wave_passes_its_patch_list.)
     if (a.tail_scatter) {
       const uint32_t tiles = (a.n + kWave - 1) / kWave;
-      // (a pool block of bt >= SW tiles has bt + (parts - 1) * SW units, and its
-      // waves' lists hold SW * PT: so at most SW * (PT - parts + 1) tiles -- the
-      // jumbo shape's 16-unit lists with quarters hold 104 tiles, not the 120 of
-      // SW * (PT - 1), which only a device of fewer than ~160 CUs reaches)
-      constexpr uint32_t per_block = pooled_split(SW) ? SW * (PT - pool_parts(W) + 1) : SW * PT;
+      // (a pool block of bt >= k * SW tiles has bt + (parts - 1) * k * SW units,
+      // k * SW of them split, and its waves' lists hold SW * PT: so at most
+      // SW * (PT - (parts - 1) * k) tiles -- the jumbo shape's 16-unit lists with
+      // the last 2 SW tiles in quarters hold 80 tiles (64 at 1M frames on 256
+      // CUs); until round 5 the bound was SW * (PT - 1), 120)
+      constexpr uint32_t per_block = pooled_split(SW) ? SW * (PT - (pool_parts(W) - 1) * pool_split_k(W)) : SW * PT;
       const uint32_t fit = (tiles + per_block - 1) / per_block;
       if (grid < fit) grid = fit;
     }
