@@ -1171,7 +1171,10 @@ constexpr bool pooled_split(int sw) { return sw > kWavesPerBlock; }
 // interleaved round faster, NIC -1..-2 us; as many as the lists hold, leaving
 // the waves no slack to balance: +50 us -- ab_jumbo_split_tiles_r05jk.jsonl).
 constexpr uint32_t pool_parts(int w) { return w == 4 ? 4u : 2u; }
-constexpr uint32_t pool_split_k(int w) { return w == 4 ? 2u : 1u; }
+// Tiles split at the end of a pool block of SW waves (the last 8 or 16 tiles
+// halved instead of 12 at 1500 B: 276.5-277.5 and 277.5-278.5 vs 277.3-278.3
+// us, NIC +0.5..1 -- profiles/r05/ab/ab_halves_tiles_*).
+constexpr uint32_t pool_split_tiles(int w, int sw) { return w == 4 ? 2u * sw : static_cast<uint32_t>(sw); }
 
 // The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
 // a 16-unit list (64 KiB of its block's 135 KiB): with every check deferred
@@ -1338,7 +1341,7 @@ void checksum_kernel_split(const KernelArgs args) {
   // stream for ~160 us each.  (Whole tiles only: IMIX level, 1500 B +6-7 us;
   // profiles/r04/ab/ab_pool_no_halves*.)
   constexpr uint32_t kParts = pool_parts(W);
-  const uint32_t nsplit = kPool ? min(bt, pool_split_k(W) * static_cast<uint32_t>(SW)) : 0u;
+  const uint32_t nsplit = kPool ? min(bt, pool_split_tiles(W, SW)) : 0u;
   const uint32_t nfull = bt - nsplit;
   const uint32_t units = nfull + kParts * nsplit;
   const auto pool_unit = [&](uint32_t p) { return p < units ? p : kNoTile; };
@@ -2156,7 +2159,7 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
       // SW * (PT - (parts - 1) * k) tiles -- the jumbo shape's 16-unit lists with
       // the last 2 SW tiles in quarters hold 80 tiles (64 at 1M frames on 256
       // CUs); until round 5 the bound was SW * (PT - 1), 120)
-      constexpr uint32_t per_block = pooled_split(SW) ? SW * (PT - (pool_parts(W) - 1) * pool_split_k(W)) : SW * PT;
+      constexpr uint32_t per_block = pooled_split(SW) ? SW * PT - (pool_parts(W) - 1) * pool_split_tiles(W, SW) : SW * PT;
       const uint32_t fit = (tiles + per_block - 1) / per_block;
       if (grid < fit) grid = fit;
     }
