@@ -759,7 +759,15 @@ def main():
             r["probes"] = probes_for(r)
         sec[name] = step_summary(r, args.steps)
         del r
-        torch.cuda.empty_cache()
+        # A workload's freed buffers stay in torch's cache for the next one: a
+        # batch allocated from the driver again after a 27 GB free (the 64 B
+        # workload's 13 rotated batches) streams slower than the same batch in
+        # memory allocated first -- jumbo 1474 vs 1452-1456 us, config 4 910 vs
+        # 887, IMIX 113.5 vs 110.8 (profiles/r05/ab/ab_bench_alloc_*.jsonl); an
+        # NF allocates its UMEM once, at start.  (XSKNF_BENCH_EMPTY_CACHE=1: the
+        # round-4 behaviour, for A/B.)
+        if os.environ.get("XSKNF_BENCH_EMPTY_CACHE"):
+            torch.cuda.empty_cache()
 
     root_scatter = root_scatter_leg(args, world, rank, dev) if (_DIST and not args.no_root_scatter) else None
     # what the collectives saw: every rank contributes 1 (so a SCALE line shows
