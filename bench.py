@@ -763,8 +763,9 @@ def main():
         # batch allocated from the driver again after a 27 GB free (the 64 B
         # workload's 13 rotated batches) streams slower than the same batch in
         # memory allocated first -- jumbo 1474 vs 1452-1456 us, config 4 910 vs
-        # 887, IMIX 113.5 vs 110.8 (profiles/r05/ab/ab_bench_alloc_*.jsonl); an
-        # NF allocates its UMEM once, at start.  (XSKNF_BENCH_EMPTY_CACHE=1: the
+        # 887, IMIX 113.5 vs 110.8; the 13M-frame 64 B batch the other way, 640
+        # vs 659 (profiles/r05/ab/ab_bench_alloc_*.jsonl): every workload runs
+        # on first-allocated memory, as an NF's UMEM, allocated once at start.  (XSKNF_BENCH_EMPTY_CACHE=1: the
         # round-4 behaviour, for A/B.)
         if os.environ.get("XSKNF_BENCH_EMPTY_CACHE"):
             torch.cuda.empty_cache()
