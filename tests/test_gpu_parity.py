@@ -995,7 +995,7 @@ TL_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 @pytest.mark.skipif(not os.path.exists(TL_LIB), reason="timeline build absent (make tl)")
 @pytest.mark.parametrize("frames_n,bpc", [(600_000, 1), (1 << 20, 1), (1 << 20, 8)])
-@pytest.mark.parametrize("window,limit", [(24, 6), (56, 7), (52, 16)], ids=["static", "pool", "pool-jumbo"])
+@pytest.mark.parametrize("window,limit", [(24, 6), (56, 7), (52, 20)], ids=["static", "pool", "pool-jumbo"])
 def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
     """launch_split sizes the grid so that no wave of a patch-list shape gets
     more tiles than its list holds (static: each wave's share of the tiles;
@@ -1024,10 +1024,10 @@ def test_no_wave_passes_its_patch_list(dev, window, limit, frames_n, bpc):
 def test_grid_sizing_on_a_smaller_device(length, n, window):
     """launch_split's grid on a device of 4 CUs (XSKNF_GPU_CU_LIMIT, a test hook
     read once per process, hence the child): a pool block of bt tiles has
-    bt + (parts - 1) * k * SW units, so a jumbo block (its last 2 SW tiles in
-    quarters, 8 waves of 16-unit lists) holds 80 tiles, not SW * (PT - 1) = 120
-    (round 4's bound; 104 with the last SW tiles split) -- at 4 x 120 and
-    4 x 104 tiles the grid must grow past 4 blocks, and every frame still
+    bt + (parts - 1) * k * SW units, so a jumbo block (its last 3 SW tiles in
+    quarters, 8 waves of 20-unit lists) holds 88 tiles, not SW * (PT - 1) -- at
+    4 x 120 and 4 x 104 tiles (round 4's bound with 16-unit lists, and 104 with
+    the last SW tiles split) the grid must grow past 4 blocks, and every frame still
     bit-exact.  The pooled W = 8, static and lane shapes at (or past)
     their bounds at 4 CUs too."""
     import json

@@ -1166,23 +1166,26 @@ constexpr bool pooled_split(int sw) { return sw > kWavesPerBlock; }
 // The parts each of a pool block's last tiles runs as: halves up to 4 KiB,
 // quarters for jumbo (W = 4; halves 1469.5-1470.7, eighths 1471.1-1471.5 vs
 // 1459.2-1461.0 us, NIC +10..14 us -- profiles/r05/ab/ab_jumbo_parts_r05jp.jsonl),
-// and how many: the last SW tiles, the last 2 SW for jumbo (1445.2-1445.7 vs
-// 1447.9-1448.8 us and 1455.4-1456.3 vs 1456.4-1459.2 on a second box, every
-// interleaved round faster, NIC -1..-2 us; as many as the lists hold, leaving
-// the waves no slack to balance: +50 us -- ab_jumbo_split_tiles_r05jk.jsonl).
+// and how many: the last SW tiles, the last 3 SW for jumbo (2 SW with 16-unit
+// lists: 1445.2-1445.7 vs 1447.9-1448.8 us and 1455.4-1456.3 vs 1456.4-1459.2
+// on a second box, NIC -1..-2, ab_jumbo_split_tiles_r05jk.jsonl; 3 SW with
+// 20-unit lists: NIC -3.5..-4 us on two boxes, worst case -0.5..-1.7,
+// ab_jumbo_units20_r05j20.jsonl; as many as the lists hold, leaving the waves
+// no slack to balance: +50 us).
 constexpr uint32_t pool_parts(int w) { return w == 4 ? 4u : 2u; }
 // Tiles split at the end of a pool block of SW waves (the last 8 or 16 tiles
 // halved instead of 12 at 1500 B: 276.5-277.5 and 277.5-278.5 vs 277.3-278.3
 // us, NIC +0.5..1 -- profiles/r05/ab/ab_halves_tiles_*).
-constexpr uint32_t pool_split_tiles(int w, int sw) { return w == 4 ? 2u * sw : static_cast<uint32_t>(sw); }
+constexpr uint32_t pool_split_tiles(int w, int sw) { return w == 4 ? 3u * sw : static_cast<uint32_t>(sw); }
 
 // The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
-// a 16-unit list (64 KiB of its block's 135 KiB): with every check deferred
+// a 20-unit list (80 KiB of its block's 151 KiB; 16 units until the late
+// round-5 A/B above): with every check deferred
 // (fused_stores 2 + 16) the block's queue patches them in the launch instead of
 // a scatter_checks pass (round 5: 9000 B 1448.4-1449.3 vs 1455.9-1457.9 us and
 // 1457.2-1458.1 vs 1461.6-1462.9 on a second box, NIC checks -4 us;
 // profiles/r05/ab/).
-constexpr int kJumboPatchUnits = 16;
+constexpr int kJumboPatchUnits = 20;
 template <int W, int NCH, int U, bool kPool>
 constexpr int patch_list_tiles() {
   if constexpr (W == 4 && NCH == 3 && U >= 2 && kPool) return kJumboPatchUnits;
@@ -1281,7 +1284,7 @@ void checksum_kernel_split(const KernelArgs args) {
   __shared__ __attribute__((aligned(16))) uint16_t itemq[SW][kItemCap];
   __shared__ __attribute__((aligned(16))) uint4 meta[SW][kWave];
   __shared__ __attribute__((aligned(16))) uint32_t accb[SW][kWave];
-  // (jumbo's 16-unit list: each wave patching its own list after its last unit tied the scatter
+  // (jumbo's list: each wave patching its own list after its last unit tied the scatter
   // pass, 1463 vs 1461 us -- profiles/r02/ab_jumbo_tail.jsonl; from the block's queue it is ahead)
   constexpr int PT = patch_list_tiles<W, NCH, U, kPool>();
   __shared__ __attribute__((aligned(16))) uint2 plist[SW][PT > 0 ? PT * kWave : 1];
@@ -2156,8 +2159,8 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
       const uint32_t tiles = (a.n + kWave - 1) / kWave;
       // (a pool block of bt >= k * SW tiles has bt + (parts - 1) * k * SW units,
       // k * SW of them split, and its waves' lists hold SW * PT: so at most
-      // SW * (PT - (parts - 1) * k) tiles -- the jumbo shape's 16-unit lists with
-      // the last 2 SW tiles in quarters hold 80 tiles (64 at 1M frames on 256
+      // SW * (PT - (parts - 1) * k) tiles -- the jumbo shape's 20-unit lists with
+      // the last 3 SW tiles in quarters hold 88 tiles (64 at 1M frames on 256
       // CUs); until round 5 the bound was SW * (PT - 1), 120)
       constexpr uint32_t per_block = pooled_split(SW) ? SW * PT - (pool_parts(W) - 1) * pool_split_tiles(W, SW) : SW * PT;
       const uint32_t fit = (tiles + per_block - 1) / per_block;
