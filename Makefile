@@ -21,7 +21,7 @@ ASM := build/asm/checksummer-gfx950.s
 # The library is kept only if the device code passes tools/check_inflight.py:
 # no instruction may name a register of an inline-asm load before its counted
 # s_waitcnt (the compiler does not know those registers are still in flight).
-$(LIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h tools/check_inflight.py Makefile
+$(LIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h xsknf_amd/csrc/checksummer_ab.h tools/check_inflight.py Makefile
 	@mkdir -p $(LIBDIR) build/asm
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o $(ASM) xsknf_amd/csrc/checksummer.hip
 	python3 tools/check_inflight.py $(ASM)
@@ -42,7 +42,13 @@ PROBELIB := tools/build/libhbm_probe.so
 HOOKBENCH := tools/build/hook_bench
 CTXLAT := tools/build/ctx_latency
 BARPROBE := tools/build/bar_probe
-tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH) $(CTXLAT) $(BARPROBE)
+DEVPROBE := tools/build/dev_probe
+tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH) $(CTXLAT) $(BARPROBE) $(DEVPROBE)
+# one NF-shaped process start (device count, a context), for tools/nf_start_probe.py
+$(DEVPROBE): tools/dev_probe.c $(LIB)
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -o $@ $< -L$(LIBDIR) -lxsknf_gpu \
+		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 $(BARPROBE): tools/bar_probe.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
@@ -74,7 +80,7 @@ $(CTXLAT): tools/ctx_latency.c $(LIB)
 # XSKNF_GPU_LIB=build/ab/libxsknf_gpu.so selects it).  Not the product.
 ABLIB := build/ab/libxsknf_gpu.so
 ab: $(ABLIB)
-$(ABLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h tools/check_inflight.py Makefile
+$(ABLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h xsknf_amd/csrc/checksummer_ab.h tools/check_inflight.py Makefile
 	@mkdir -p build/ab
 	$(HIPCC) $(HIPFLAGS) -DXSKNF_AB --cuda-device-only -S -o build/ab/checksummer-gfx950.s xsknf_amd/csrc/checksummer.hip
 	python3 tools/check_inflight.py build/ab/checksummer-gfx950.s
@@ -84,7 +90,7 @@ $(ABLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h tool
 # samples (tools/timeline.py).  Not the product.
 TLLIB := build/tl/libxsknf_gpu.so
 tl: $(TLLIB)
-$(TLLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h tools/check_inflight.py Makefile
+$(TLLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h xsknf_amd/csrc/checksummer_ab.h tools/check_inflight.py Makefile
 	@mkdir -p build/tl
 	$(HIPCC) $(HIPFLAGS) -DXSKNF_TIMELINE $(TLFLAGS) --cuda-device-only -S -o build/tl/checksummer-gfx950.s xsknf_amd/csrc/checksummer.hip
 	python3 tools/check_inflight.py build/tl/checksummer-gfx950.s

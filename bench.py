@@ -200,6 +200,16 @@ def allreduce_max(x: float, world: int) -> float:
     return float(t.item())
 
 
+def allgather_f64(vals, world):
+    """Every rank's `vals` (a list of floats), as a list per rank (rank order)."""
+    t = torch.tensor(vals, dtype=torch.float64, device=coll_device())
+    if not _DIST:
+        return [t.tolist()]
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.tolist() for p in parts]
+
+
 def allreduce_sum_i64(vals, world):
     t = torch.tensor(vals, dtype=torch.int64, device=coll_device())
     if _DIST:
@@ -367,6 +377,9 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     step_ms = (sum(a.elapsed_time(b) for a, b in evs) if nic else ev0.elapsed_time(ev1)) / args.steps
     wall_max = allreduce_max(wall, world)
     step_ms_max = allreduce_max(step_ms, world)
+    # every rank's own step (HIP events) and wall time, and its bytes: a straggler
+    # rank shows in the line (dist.per_rank), not only in the max
+    per_rank = allgather_f64([step_ms, wall / args.steps * 1e3, float(bytes_len), float(n)], world)
     if not nic:
         # leave batch 0 as one -i 1 pass leaves it (the CPU leg checks it)
         cs.process_batch_ptr(umem_ptr, umem_size, descs_ptrs[0], n, v_ptrs[0], 0, stream.cuda_stream)
@@ -433,7 +446,7 @@ def time_workload(name, args, world, rank, dev, seed, primary):
     return dict(name=name, desc=desc, n=n, K=K, lens=lens, bytes_len=bytes_len, step_ms=step_ms, stores=stores,
                 rfc=rfc,
                 shape=shape,
-                step_ms_max=step_ms_max,
+                step_ms_max=step_ms_max, per_rank=per_rank,
                 sum_ms=k_ms, single_kernel=single_kernel, family=family, wall_max=wall_max, counters=counters,
                 umem=umem, descs=descs, verdicts=verdicts, sample=sample, layout=layout, chunk=chunk, span=span)
 
@@ -776,8 +789,21 @@ def main():
     dist_info = None
     if _DIST:
         seen = allreduce_sum_i64([1], world)[0]
+        pr = prim["per_rank"]
+        steps_us = [round(r[0] * 1e3, 2) for r in pr]
+        walls_ms = [round(r[1], 4) for r in pr]
+        rates = [r[2] / (r[0] / 1e3) / 1e9 for r in pr]          # each rank's GB/s on its own step
         dist_info = {"ranks_seen": seen, "backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
                      "frames_allreduced": prim["counters"][0],
+                     "per_rank": {"step_us": steps_us, "wall_ms_per_step": walls_ms,
+                                  "gbs_checksummed": [round(x, 1) for x in rates],
+                                  "frames": [int(r[3]) for r in pr]},
+                     "step_us_min": min(steps_us), "step_us_max": max(steps_us),
+                     "step_spread": round(max(steps_us) / min(steps_us), 4) if min(steps_us) > 0 else None,
+                     # the rate one rank reaches alone (its N = 1 equivalent), and the sum of the
+                     # ranks' own rates: value / that sum < 1 is what the max-over-ranks clock cost
+                     "per_rank_gbs_mean": round(sum(rates) / len(rates), 1),
+                     "sum_of_rank_rates_gbs": round(sum(rates), 1),
                      "collective_device": coll_device(),
                      "collectives": "barrier + max-time and counter all-reduces after the timed region; "
                                     "root_scatter: broadcast + point-to-point isend/irecv"}
@@ -799,10 +825,15 @@ def main():
                         "us": round(prim["sum_ms"] * 1e3, 2), "alg_bytes": alg_k,
                         "achieved": round(alg_k / (prim["sum_ms"] / 1e3) / 1e9, 1),
                         "frac": round(alg_k / (prim["sum_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    # the same bytes over `value`'s clock (wall time around the K steps, max over ranks, per rank)
+    achieved_wall = step_alg / step_s / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_for(args.workload),
-            "basis": "whole step (SURVEY.md 8(d)): sum(len + 22) per batch / HIP-event step time on the launch "
-                     "stream; traffic = FETCH_SIZE/WRITE_SIZE of every kernel of one step",
+            "basis": "frac / achieved: whole step (SURVEY.md 8(d)), sum(len + 22) per batch on rank 0 / the "
+                     "step's HIP-event time on the launch stream (the kernels' own time); frac_wall / "
+                     "achieved_wall: the same bytes over value's time base (wall clock around the timed steps, "
+                     "max over ranks); traffic = FETCH_SIZE/WRITE_SIZE of every kernel of one step",
+            "achieved_wall": round(achieved_wall, 1), "frac_wall": round(achieved_wall / HBM_PEAK_GBS, 4),
             "kernels": f"{prim['family']} ({prim['stores']})", "launch_shape": prim["shape"],
             "alg_bytes_per_step": step_alg, "step_us": round(step_k_s * 1e6, 2),
             "summing_kernel_alone": kernel_alone,

@@ -82,8 +82,16 @@ XSKNF_GPU_API int xsknf_gpu_device_count(int *count);
  * of the same bytes order-dependent; here their frames are checksummed
  * concurrently).
  * A batch runs as one launch per 1M frames (per 16M for frames of at most
- * 128 bytes, where one launch over more frames measured faster).
+ * 128 bytes, where one launch over more frames measured faster; a lane-kernel
+ * launch of more than 2M frames loads each lane's window itself and runs 8
+ * blocks per CU, the faster shape for a long launch -- for the default shape
+ * only: xsknf_gpu_checksum_batch_cfg() with blocks_per_cu != 0 runs exactly
+ * the shape it is given).
  * Returns 0, -EINVAL on bad arguments, -EIO on a HIP launch error.
+ *
+ * Test hook: the environment variable XSKNF_GPU_CU_LIMIT=N sizes every grid as
+ * on a device of N CUs (results are unchanged, launches slower; the library
+ * says so on stderr once per device).  Not for production use.
  */
 XSKNF_GPU_API int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size,
 		const struct xsknf_gpu_desc *descs, uint32_t n,

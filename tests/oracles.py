@@ -1,20 +1,27 @@
 """The CPU answer the full-size GPU parity tests compare with (test infrastructure).
 
-Where `oracle/_ref/libcsum_ref.so` was built (the reference's own
-xsknf_packet_processor(), checksummer_user.c:30-112 compiled from its verbatim
-lines; it travels to the GPU box as a built library), the full-size runs are
-held against the reference itself, in process_batch_1if()'s batch-64 loop
-(src/xsknf.c:654-672) split over threads; elsewhere against the restatement
-oracle/csum_oracle.c, which tests/test_ref_pin.py holds equal to it.
+`oracle/_ref/libcsum_ref.so` is the reference's own xsknf_packet_processor()
+(checksummer_user.c:30-112 compiled from its verbatim lines; built by build()
+wherever the reference checkout exists, it travels to the GPU box as a built
+library).  The full-size runs are held against it, in process_batch_1if()'s
+batch-64 loop (src/xsknf.c:654-672) split over threads.  It is required: a GPU
+run without it fails (there is no quiet fall back to the restatement, which
+tests/test_ref_pin.py holds equal to it on CPU).
 """
-from oracle import csum_oracle as O
 from oracle import ref as R
 
-KIND = "reference" if R.available() else "restatement"
+KIND = "reference"
+
+
+def require():
+    """Fail loudly when the reference library is not here."""
+    if not R.available():
+        raise RuntimeError(f"{R.LIB_PATH} is missing: build it with `make oracle` in a container that holds the "
+                           "reference checkout (build() does); the GPU parity tests compare with it, not with "
+                           "the restatement")
 
 
 def time_batch(umem, descs, threads=16, **kw):
     """In place over the host batch; returns (seconds, verdicts)."""
-    if R.available():
-        return R.time_batch(umem, descs, threads=threads, reps=1, pin=False, **kw)
-    return O.c_time_batch(umem, descs, threads=threads, reps=1, **kw)
+    require()
+    return R.time_batch(umem, descs, threads=threads, reps=1, pin=False, **kw)

@@ -173,6 +173,16 @@ def test_bench_gpus_n_starts_its_ranks(dev, clean_ctx, world):
     # distribution ran by default and delivered every frame
     assert line["dist"]["ranks_seen"] == world and line["dist"]["world_size"] == world
     assert line["dist"]["frames_allreduced"] == world * 65536
+    # every rank's own step is in the line (a straggler is visible), consistent with the max
+    pr = line["dist"]["per_rank"]
+    assert len(pr["step_us"]) == world and len(pr["wall_ms_per_step"]) == world
+    assert pr["frames"] == [65536] * world and all(x > 0 for x in pr["gbs_checksummed"])
+    assert line["dist"]["step_us_max"] == max(pr["step_us"]) and line["dist"]["step_us_min"] == min(pr["step_us"])
+    assert line["dist"]["step_spread"] >= 1.0
+    assert line["dist"]["sum_of_rank_rates_gbs"] >= line["dist"]["per_rank_gbs_mean"] > 0
+    assert abs(line["ms_per_step"] - max(pr["wall_ms_per_step"])) <= 1e-3 * max(1.0, line["ms_per_step"])
+    # both time bases of the roofline, named
+    assert 0 < line["roofline"]["frac_wall"] and "frac_wall" in line["roofline"]["basis"]
     assert line["root_scatter"]["frames_total"] == world * 65536
     assert line["root_scatter"]["vs_single_gpu"]["match"] is True
     assert line["root_scatter"]["rfc_check"]["violations"] == 0

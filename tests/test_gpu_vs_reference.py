@@ -9,7 +9,7 @@ with the library itself, through the C ABI, on seeded randomized batches that
 cover every branch of :34-55, odd starts, iterations -3..7919, both actions,
 1-4 interfaces, every launch family (lane kernel, split kernel with and
 without the pool, jumbo) and the three host paths.  Bit-exact: every verdict
-and every UMEM byte.  Skipped where the library was not built.
+and every UMEM byte.  A GPU run without the library fails (it is not skipped).
 """
 import numpy as np
 import pytest
@@ -26,8 +26,8 @@ torch = pytest.importorskip("torch")
 def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    if not R.available():
-        pytest.skip("oracle/_ref not built (no reference checkout where this tree was built)")
+    if not R.available():   # required on a GPU box (tests/oracles.py): no skip
+        pytest.fail(f"{R.LIB_PATH} not built: run build() where the reference checkout exists")
     return torch.device("cuda:0")
 
 

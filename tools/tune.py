@@ -5,7 +5,8 @@ rounds, median of per-round HIP-event timings), on device-resident batches.
     python tools/tune.py --workload 1500 --variants 32,3,2:32,3,1:64,2,1:32,3,1,3 [--bpc 8,4]
 
 A variant is lanes_per_frame,chunks_per_lane,frames_per_group[,lds_ring[,fused_stores[,kernel,window]]]
-(lds_ring > 0 selects the LDS-DMA kernel; fused_stores 1 = single-pass stores;
+(lds_ring must be 0: the LDS-DMA kernels were removed in round 5 and any other value is
+-EINVAL; fused_stores 1 = single-pass stores;
 kernel 1 = the split kernel with a `window`-chunk header window per lane).
 
 Every variant's output (verdicts + whole UMEM) is compared with the default

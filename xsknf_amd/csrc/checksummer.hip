@@ -51,6 +51,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dirent.h>
+#include <stdarg.h>
+#include <fcntl.h>
+#include <unistd.h>
 
 #include "../../include/xsknf_gpu.h"
 #include "checksummer_internal.h"
@@ -2003,13 +2007,29 @@ __global__ __launch_bounds__(kBlock) void resident_kernel(const ResArgs ra) {
 
 // ---- host side ----------------------------------------------------------------
 
+}  // namespace xsknf_gpu
+
+// A/B builds (make ab) add launch shapes and knobs; the product sees no-ops
+#ifdef XSKNF_AB
+#include "checksummer_ab.h"
+#else
+namespace xsknf_gpu {
+inline void ab_note_occupancy(const void *, int, int) {}
+inline int ab_scatter_bpc(int dflt) { return dflt; }
+inline bool ab_no_grid_bound() { return false; }
+}  // namespace xsknf_gpu
+#define XSKNF_AB_VARIANTS
+#endif
+
+namespace xsknf_gpu {
+
 // The last error of ANY thread: a worker thread's failure (hook context
 // creation, UMEM registration, a launch) must be readable by the application's
 // main thread (checksummer_app.c prints it).  Each reader gets a private copy,
 // so the returned text cannot change under it.
 std::mutex g_err_mu;
-char g_last_error[256] = "";
-thread_local char g_err_copy[256] = "";
+char g_last_error[1024] = "";
+thread_local char g_err_copy[1024] = "";
 
 void set_error_text(const char *text) {
   std::lock_guard<std::mutex> lk(g_err_mu);
@@ -2027,6 +2047,74 @@ const char *last_error_copy() {
   return g_err_copy;
 }
 
+// A process that finds no usable device says why (src/xsknf.c:108-119: a start
+// failure is fatal and loud): HIP's error and count, whether this process can
+// open the KFD and the first render node, which *_VISIBLE_DEVICES are set, how
+// many processes hold a KFD context (/sys/class/kfd/kfd/proc, by pid) and this
+// process's open descriptors.  Used where hipGetDeviceCount fails or sees none.
+struct ErrText {
+  char buf[sizeof(g_last_error)] = "";
+  size_t o = 0;
+  __attribute__((format(printf, 2, 3))) void put(const char *fmt, ...) {
+    if (o >= sizeof(buf)) return;
+    va_list ap;
+    va_start(ap, fmt);
+    const int w = vsnprintf(buf + o, sizeof(buf) - o, fmt, ap);
+    va_end(ap);
+    if (w > 0) o += static_cast<size_t>(w);
+  }
+};
+
+int set_device_error(hipError_t e, int count, const char *where) {
+  ErrText t;
+  t.put("%s: %s (hipError %d), %d devices", where, hipGetErrorString(e), static_cast<int>(e), count);
+  const int kfd = open("/dev/kfd", O_RDWR | O_CLOEXEC);
+  if (kfd >= 0) {
+    t.put("; /dev/kfd opens");
+    close(kfd);
+  } else {
+    t.put("; /dev/kfd: errno %d (%s)", errno, strerror(errno));
+  }
+  int render = 0;
+  char first[64] = "";
+  if (DIR *d = opendir("/dev/dri")) {
+    while (const dirent *ent = readdir(d))
+      if (!strncmp(ent->d_name, "renderD", 7) && render++ == 0) snprintf(first, sizeof(first), "%s", ent->d_name);
+    closedir(d);
+  }
+  if (render) {
+    char path[96];
+    snprintf(path, sizeof(path), "/dev/dri/%s", first);
+    const int fd = open(path, O_RDWR | O_CLOEXEC);
+    t.put("; %d render nodes, %s %s", render, path, fd >= 0 ? "opens" : strerror(errno));
+    if (fd >= 0) close(fd);
+  } else {
+    t.put("; no render node in /dev/dri");
+  }
+  for (const char *v : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
+    if (const char *s = getenv(v)) t.put("; %s=%s", v, s);
+  int procs = 0;
+  if (DIR *d = opendir("/sys/class/kfd/kfd/proc")) {
+    t.put("; KFD processes:");
+    while (const dirent *ent = readdir(d))
+      if (ent->d_name[0] != '.') {
+        if (procs++ < 16) t.put(" %s", ent->d_name);
+      }
+    closedir(d);
+    t.put(" (%d; this pid %d)", procs, static_cast<int>(getpid()));
+  } else {
+    t.put("; /sys/class/kfd/kfd/proc: %s", strerror(errno));
+  }
+  int fds = 0;
+  if (DIR *d = opendir("/proc/self/fd")) {
+    while (const dirent *ent = readdir(d)) fds += ent->d_name[0] != '.';
+    closedir(d);
+  }
+  t.put("; %d open fds", fds);
+  set_error_text(t.buf);
+  return -ENODEV;
+}
+
 int device_cus() {
   static int cache[64];
   int dev = 0;
@@ -2040,7 +2128,12 @@ int device_cus() {
     // smaller devices are exercised on this one (tests/test_gpu_parity.py)
     if (const char *lim = getenv("XSKNF_GPU_CU_LIMIT")) {
       const int l = atoi(lim);
-      if (l > 0 && l < cus) cus = l;
+      if (l > 0 && l < cus) {
+        // a stray value would quietly slow every launch: say so, once per device
+        fprintf(stderr, "libxsknf_gpu: XSKNF_GPU_CU_LIMIT=%d (test only): grids sized for %d of device %d's %d CUs\n",
+                l, l, dev, cus);
+        cus = l;
+      }
     }
     cache[dev] = cus;
   }
@@ -2061,9 +2154,7 @@ int resident_blocks(const void *kernel, int threads) {
     if (cache[i].k == kernel && cache[i].dev == dev) return cache[i].blocks;
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, threads, 0) != hipSuccess || b <= 0) b = 1;
-#ifdef XSKNF_AB
-  if (getenv("XSKNF_AB_OCCUPANCY")) fprintf(stderr, "occupancy %p x %d threads: %d blocks per CU\n", kernel, threads, b);
-#endif
+  ab_note_occupancy(kernel, threads, b);
   if (used < 64) cache[used++] = Entry{kernel, dev, b};
   return b;
 }
@@ -2093,11 +2184,7 @@ int finish_launch(const KernelArgs &a, hipStream_t stream, const char *what) {
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && a.defer_min_len != kNoDefer && !a.no_scatter && !a.tail_scatter) {
     const uint32_t need = (4 * a.n + kBlock - 1) / kBlock;   // dense shape: 4 lanes per frame
-    int bpc = 8;   // scatter blocks per CU
-#ifdef XSKNF_AB
-    static const int ab_bpc = getenv("XSKNF_SCATTER_BPC") ? atoi(getenv("XSKNF_SCATTER_BPC")) : 8;
-    bpc = ab_bpc > 0 ? ab_bpc : 8;
-#endif
+    const int bpc = ab_scatter_bpc(8);   // scatter blocks per CU
     const uint32_t cap = static_cast<uint32_t>(device_cus() * bpc);
     hipLaunchKernelGGL(scatter_checks, dim3(need < cap ? need : cap), dim3(kBlock), 0, stream, a);
     e = hipGetLastError();
@@ -2186,16 +2273,8 @@ struct Variant {
 
 #define XSKNF_V(L, N, S) {L, N, S, 0, &launch_reg<L, N, S>}
 #define XSKNF_L(N, S) {1, N, S, 0, &launch_lane<N, S>}
-// lane kernel, one 16-wave block per CU with the tile pool (window field 32)
-#define XSKNF_LP(N, S) {1, N, S, 0, &launch_lane<N, S, 16>, XSKNF_GPU_KERNEL_AUTO, 32}
-// lane kernel with the transposed (coalesced) window load (window field 512)
-#define XSKNF_LT(N, S) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, 1, 1>, XSKNF_GPU_KERNEL_AUTO, 512}
 // ... transposed per tile where the tile's frames lie apart (window field 1024)
 #define XSKNF_LA(N, S) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, 4, 2>, XSKNF_GPU_KERNEL_AUTO, 1024}
-// (A/B) the pooled lane kernel with the per-tile transposed windows (window field 1056)
-#define XSKNF_LPA(N, S) {1, N, S, 0, &launch_lane<N, S, 16, 4, 2>, XSKNF_GPU_KERNEL_AUTO, 1056}
-// (A/B) lane kernel held to WPE waves per SIMD (window field 64 + 256 * WPE)
-#define XSKNF_LW(N, S, WPE) {1, N, S, 0, &launch_lane<N, S, kWavesPerBlock, WPE>, XSKNF_GPU_KERNEL_AUTO, 64 + 256 * WPE}
 // split: window field = W, + 16 for the transposed (coalesced) window load
 #define XSKNF_S(W, L, N, U, TL) {L, N, U, 0, &launch_split<W, L, N, U, TL>, XSKNF_GPU_KERNEL_SPLIT, W + 16 * TL}
 // one 12-wave block per CU, its waves drawing the CU's tiles from a shared pool (window field + 32)
@@ -2211,35 +2290,7 @@ const Variant kVariants[] = {
     XSKNF_LA(5, 2), XSKNF_L(5, 2),
     // ... and the zero-copy host path's small-batch group shapes (host_path.hip)
     XSKNF_V(32, 3, 2), XSKNF_V(64, 2, 4),
-#ifdef XSKNF_AB
-    // A/B material (`make ab` -> build/ab/libxsknf_gpu.so; tools/tune.py), not in the product library
-    XSKNF_S(4, 16, 2, 2, 0), XSKNF_S(4, 16, 2, 1, 0), XSKNF_S(4, 8, 4, 2, 0), XSKNF_S(4, 32, 1, 2, 0),
-    XSKNF_S(4, 16, 4, 1, 0), XSKNF_S(5, 16, 2, 2, 0), XSKNF_S(4, 64, 2, 1, 0), XSKNF_S(4, 32, 2, 1, 0),
-    XSKNF_S(7, 16, 2, 1, 0), XSKNF_S(4, 16, 3, 1, 0), XSKNF_S(4, 8, 2, 2, 0),
-    XSKNF_S(4, 16, 2, 1, 1), XSKNF_S(4, 16, 3, 1, 1),
-    XSKNF_S(4, 16, 4, 1, 1), XSKNF_S(4, 32, 2, 1, 1), XSKNF_S(4, 32, 3, 1, 1),
-    XSKNF_S(8, 32, 3, 1, 1), XSKNF_S(8, 16, 2, 1, 1), XSKNF_S(8, 16, 4, 1, 1),
-    XSKNF_SC(16, 2, 3),   // (jumbo in one 12-wave block per CU: 1520 vs 1456 us, r02 ab_pool_jumbo; removed r05)
-    XSKNF_LP(5, 2),   // lane kernel with the tile pool: 64 B 59.65 vs 59.51 us, a tie (r02 ab_pool_lane.jsonl)
-    // ... in 64-frame units (r05 ab_lane_pool / r05c): 64 B 58.8-59.1 vs 58.5-58.7 static (both write-through),
-    // packed 64 B 37.3 vs 38.0-38.3, packed NIC 20.1-20.4 vs 22.4-22.7
-    XSKNF_LP(5, 1),
-    XSKNF_LPA(5, 1), XSKNF_LPA(5, 2),
-    // transposed window loads (r04 ab_lane_transposed*.jsonl): aligned 64 B NIC -1 us, worst case +0.3,
-    // packed (-u) frames +1 us; per tile by the frames' spread: worst case +2 us (4 waves per SIMD forced);
-    // round 5, with the write-through sectors (ab_matrix_r05l): all transposed 57.1-57.7 vs 58.2-58.8 us,
-    // packed NIC +1 us; per tile (XSKNF_LA(5, 2)) 56.7-57.1: the product's since
-    XSKNF_LT(5, 2), XSKNF_LT(4, 2), XSKNF_LT(5, 1), XSKNF_LA(5, 1),
-    XSKNF_LA(5, 4), XSKNF_LA(4, 2),   // (r05y: 62.8-63.1 and 57.3-57.9 vs 57.0-57.6 us)
-    XSKNF_S(8, 16, 3, 2, 1),   // long-frame batches: 1500 B -1..2 %; out of the product (DESIGN 3, r02 fault)
-    XSKNF_L(5, 4),     XSKNF_L(6, 2),     XSKNF_L(7, 2),
-    XSKNF_L(4, 1),     XSKNF_L(4, 2),     XSKNF_L(5, 1),   // fewer VGPRs, more waves (r03 64 B A/B)
-    XSKNF_LW(4, 1, 8), XSKNF_LW(4, 2, 6), XSKNF_LW(5, 2, 6), XSKNF_LW(5, 1, 8),
-    XSKNF_V(4, 2, 2),  XSKNF_V(4, 2, 4),
-    XSKNF_V(8, 1, 2),  XSKNF_V(8, 1, 4),  XSKNF_V(8, 1, 8),  XSKNF_V(16, 1, 4), XSKNF_V(16, 2, 4),
-    XSKNF_V(16, 2, 8), XSKNF_V(32, 2, 4), XSKNF_V(32, 3, 4), XSKNF_V(32, 3, 8),
-    XSKNF_V(64, 2, 8), XSKNF_V(64, 4, 4), XSKNF_V(64, 9, 2), XSKNF_V(64, 9, 4),
-#endif
+    XSKNF_AB_VARIANTS   // (A/B builds only: checksummer_ab.h)
 };
 #undef XSKNF_V
 #undef XSKNF_L
@@ -2358,7 +2409,7 @@ constexpr uint32_t kLaunchFrames = 1u << 20;
 constexpr uint32_t kLaneLaunchFrames = 1u << 24;
 constexpr uint32_t kLaneTransposedMaxFrames = 2u << 20;
 
-int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
+int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream, bool product_shape) {
   if (cfg.blocks_per_cu < 0 || cfg.blocks_per_cu > 64) return -EINVAL;
   // + 4: 2-byte in-line stores, + 8: plain sector stores, + 32: write unchanged checks too
   const int mode = cfg.fused_stores & 3;
@@ -2394,8 +2445,10 @@ int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream) {
   // profiles/r05/ab/ab_lane_la_r05n.jsonl: 1M frames 57.5-57.7 vs 58.3-59.0 us,
   // 13M frames in one launch 701-710 vs 655-662 us): a longer launch runs as
   // the per-lane shape.
+  // Only for the product's own shape (default_cfg, or an explicit cfg that leaves
+  // blocks_per_cu to the library): an explicit shape runs as asked.
   const Variant *longer = v;
-  if (v->kernel == XSKNF_GPU_KERNEL_AUTO && v->lpf == 1 && v->window == 1024) {
+  if (product_shape && v->kernel == XSKNF_GPU_KERNEL_AUTO && v->lpf == 1 && v->window == 1024) {
     xsknf_gpu_launch_cfg c = cfg;
     c.window_chunks = 0;
     if (const Variant *w = find_variant(c)) longer = w;
@@ -2426,7 +2479,11 @@ uint32_t xsknf_gpu_version(void) { return (0u << 16) | 1u; }
 int xsknf_gpu_device_count(int *count) {
   if (!count) return -EINVAL;
   hipError_t e = hipGetDeviceCount(count);
-  if (e != hipSuccess) { xsknf_gpu::set_error(e, "hipGetDeviceCount"); *count = 0; return -ENODEV; }
+  if (e != hipSuccess || *count < 1) {
+    const int seen = e == hipSuccess ? *count : 0;
+    *count = 0;
+    return xsknf_gpu::set_device_error(e, seen, "hipGetDeviceCount");
+  }
   return 0;
 }
 
@@ -2440,7 +2497,7 @@ int xsknf_gpu_checksum_batch(uint8_t *umem, uint64_t umem_size, const struct xsk
   if (rc != 0) return rc < 0 ? rc : 0;
   xsknf_gpu_launch_cfg cfg;
   xsknf_gpu::default_cfg(frame_len_hint ? frame_len_hint : 2048u, cfg);
-  return xsknf_gpu::run(a, cfg, stream);
+  return xsknf_gpu::run(a, cfg, stream, true);
 }
 
 int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct xsknf_gpu_desc *descs,
@@ -2450,7 +2507,7 @@ int xsknf_gpu_checksum_batch_cfg(uint8_t *umem, uint64_t umem_size, const struct
   xsknf_gpu::KernelArgs a;
   const int rc = xsknf_gpu::prepare(a, umem, umem_size, descs, n, ingress_ifindex, opts, verdicts);
   if (rc != 0) return rc < 0 ? rc : 0;
-  return xsknf_gpu::run(a, *cfg, stream);
+  return xsknf_gpu::run(a, *cfg, stream, cfg->blocks_per_cu == 0);
 }
 
 int xsknf_gpu_default_launch_cfg(uint32_t frame_len_hint, struct xsknf_gpu_launch_cfg *cfg) {
@@ -2468,7 +2525,7 @@ int xsknf_gpu_checksum_batch_lens(uint8_t *umem, uint64_t umem_size, const struc
   if (rc != 0) return rc < 0 ? rc : 0;
   xsknf_gpu_launch_cfg cfg;
   xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, cfg, frame_len_mean);
-  return xsknf_gpu::run(a, cfg, stream);
+  return xsknf_gpu::run(a, cfg, stream, true);
 }
 
 int xsknf_gpu_launch_cfg_for_lens(uint32_t frame_len_max, uint32_t frame_len_mean,

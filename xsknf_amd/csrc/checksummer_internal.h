@@ -46,10 +46,16 @@ constexpr uint32_t kNoDefer = 0xffffffffu;   // defer_min_len: every check in-li
 int prepare(KernelArgs &a, uint8_t *umem, uint64_t umem_size, const xsknf_gpu_desc *descs, uint32_t n,
             uint32_t ingress_ifindex, const xsknf_csum_opts *opts, int32_t *verdicts);
 // Launch the shape `cfg` (summing kernel + scatter pass unless a.no_scatter).
-int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream);
+// product_shape: cfg is default_cfg()'s (or leaves blocks_per_cu to the library),
+// so a lane-kernel launch of more than 2M frames may take the per-lane windows
+// and 8 blocks per CU; an explicit shape runs exactly as asked.
+int run(const KernelArgs &base, const xsknf_gpu_launch_cfg &cfg, void *stream, bool product_shape);
 void default_cfg(uint32_t hint, xsknf_gpu_launch_cfg &c, uint32_t mean = 0);
 void set_error(hipError_t e, const char *where);
 void set_error_text(const char *text);
+// hipGetDeviceCount failed or saw no device: -ENODEV, with what the process saw
+// (KFD / render node access, *_VISIBLE_DEVICES, KFD processes) as the error text
+int set_device_error(hipError_t e, int count, const char *where);
 
 // ---- the resident worker (XSKNF_GPU_PATH_RESIDENT, host_path.hip) ----------
 // ONE kernel per device stays resident and serves the rings of every RESIDENT

@@ -150,6 +150,7 @@ struct xsknf_gpu_ctx {
 namespace {
 
 int fail(hipError_t e, const char *where) {
+  if (e == hipErrorNoDevice) return xsknf_gpu::set_device_error(e, 0, where);
   xsknf_gpu::set_error(e, where);
   return -EIO;
 }
@@ -664,7 +665,7 @@ int submit_piece(xsknf_gpu_ctx *c, const xsknf_gpu_desc *descs, uint32_t n, uint
     cfg.fused_stores = 3;   // records only: the checks are applied on the host (complete())
   }
   s.host_checks = !mapped;
-  rc = run(a, cfg, s.stream);
+  rc = run(a, cfg, s.stream, true);
   if (rc != 0) return rc;
   hipError_t e = hipEventRecord(s.done, s.stream);
   if (e != hipSuccess) return fail(e, "hipEventRecord");
@@ -912,9 +913,9 @@ int xsknf_gpu_hook_create(struct xsknf_gpu_hook **out, const struct xsknf_csum_o
   if (opts->action != XSKNF_CSUM_ACTION_REDIRECT && opts->action != XSKNF_CSUM_ACTION_DROP) return -EINVAL;
   *out = nullptr;
   int devices = 0;
-  hipError_t e = hipGetDeviceCount(&devices);
-  if (e != hipSuccess) return fail(e, "hipGetDeviceCount");
-  if (devices < 1) return -ENODEV;
+  // (no device: -ENODEV, and the error text says what this process saw)
+  const int rc = xsknf_gpu_device_count(&devices);
+  if (rc) return rc;
   xsknf_gpu_hook *h = new (std::nothrow) xsknf_gpu_hook;
   if (!h) return -ENOMEM;
   h->w = new (std::nothrow) HookWorker[workers];
