@@ -4,7 +4,9 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-inline-asm -fvisibility=hidden --offload-arch=$(ARCH) -Iinclude
 LIBDIR := xsknf_amd/lib
 LIB := $(LIBDIR)/libxsknf_gpu.so
-SRCS := xsknf_amd/csrc/checksummer.hip xsknf_amd/csrc/host_path.hip
+SRCS := xsknf_amd/csrc/checksummer.hip xsknf_amd/csrc/host_path.hip xsknf_amd/csrc/multi.hip
+# RCCL for the multi-device calls (xsknf_gpu_multi_*)
+GPULIBS := -L/opt/rocm/lib -lrccl
 
 # host side: the AF_XDP runtime (plain C) and the checksummer NF binary
 CC ?= gcc
@@ -25,7 +27,7 @@ $(LIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h xsknf_
 	@mkdir -p $(LIBDIR) build/asm
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o $(ASM) xsknf_amd/csrc/checksummer.hip
 	python3 tools/check_inflight.py $(ASM)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) $(GPULIBS)
 
 $(RTLIB): $(RTSRCS) $(RTHDRS) Makefile
 	@mkdir -p $(LIBDIR)
@@ -84,7 +86,7 @@ $(ABLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h xskn
 	@mkdir -p build/ab
 	$(HIPCC) $(HIPFLAGS) -DXSKNF_AB --cuda-device-only -S -o build/ab/checksummer-gfx950.s xsknf_amd/csrc/checksummer.hip
 	python3 tools/check_inflight.py build/ab/checksummer-gfx950.s
-	$(HIPCC) $(HIPFLAGS) -DXSKNF_AB -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -DXSKNF_AB -shared -o $@ $(SRCS) $(GPULIBS)
 
 # Timeline build: the product shapes with the split kernel's per-wave clock
 # samples (tools/timeline.py).  Not the product.
@@ -94,7 +96,7 @@ $(TLLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h xskn
 	@mkdir -p build/tl
 	$(HIPCC) $(HIPFLAGS) -DXSKNF_TIMELINE $(TLFLAGS) --cuda-device-only -S -o build/tl/checksummer-gfx950.s xsknf_amd/csrc/checksummer.hip
 	python3 tools/check_inflight.py build/tl/checksummer-gfx950.s
-	$(HIPCC) $(HIPFLAGS) -DXSKNF_TIMELINE $(TLFLAGS) -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -DXSKNF_TIMELINE $(TLFLAGS) -shared -o $@ $(SRCS) $(GPULIBS)
 
 # keep the device assembly for inspection (VGPRs, instruction mix)
 asm: $(SRCS)
@@ -120,4 +122,4 @@ GDLIB := build/guard/libxsknf_gpu.so
 guard: $(GDLIB)
 $(GDLIB): $(SRCS) include/xsknf_gpu.h xsknf_amd/csrc/checksummer_internal.h Makefile
 	@mkdir -p build/guard
-	$(HIPCC) $(HIPFLAGS) -DXSKNF_GUARD -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) -DXSKNF_GUARD -shared -o $@ $(SRCS) $(GPULIBS)

@@ -106,6 +106,8 @@ def parse():
                    help="N > 1: skip the distribution of a root-resident global IMIX batch (SURVEY 8(e) "
                         "collective 1, reported as `root_scatter`; timed by default when N > 1)")
     p.add_argument("--no-probes", action="store_true", help="skip the read / step-floor probes")
+    p.add_argument("--no-c-host-multi", action="store_true",
+                   help="world 1: skip config 4 through the C host's multi-device calls (`c_host_multi`)")
     p.add_argument("--no-verify", action="store_true",
                    help="skip the RFC receive-side check of the primary and config4 outputs (rfc_check)")
     p.add_argument("--rotate", type=int, default=0,
@@ -529,6 +531,62 @@ def root_scatter_leg(args, world, rank, dev):
             "layout": "IMIX 64/570/1500 (7:4:1) packed, unaligned-mode descriptors; shards by bytes"}
 
 
+def c_host_multi_leg(args, dev, reps=10):
+    """BASELINE config 4 through the C host's multi-device calls (include/xsknf_gpu.h
+    xsknf_gpu_multi_*, xsknf_amd/csrc/multi.hip) in THIS one process, over every
+    visible device (XSKNF_BENCH_MULTI_DEVICES caps it): the global IMIX batch in
+    device 0's HBM, split by bytes, every shard moved by grouped RCCL ncclSend /
+    ncclRecv (device 0's own shard as a send to itself), checksummed on every
+    device at once, the counters summed by ncclAllReduce and held against one
+    device's pass over the whole batch.  At world 1 only (the ranks of
+    `--gpus N` are the one-process-per-GPU path); on a one-GPU box it runs at
+    N = 1."""
+    from xsknf_amd import multi
+    ndev = torch.cuda.device_count()
+    if os.environ.get("XSKNF_BENCH_MULTI_DEVICES"):
+        ndev = max(1, min(ndev, int(os.environ["XSKNF_BENCH_MULTI_DEVICES"])))
+    n = args.config4_frames
+    umem, dt, lens = frames.device_batch(n, "imix", layout="aligned", chunk=frames.CHUNK, seed=frames.SEED,
+                                         device=dev)
+    hd = dt.cpu().numpy().view(frames.DESC_DTYPE).reshape(-1).copy()
+    mean = int(lens.mean())
+    total = int(lens.astype(np.int64).sum())
+    opts = [ChecksummerOptions(csum_iterations=i) for i in (1, 2)]
+    with multi.MultiDevice(range(ndev)) as m:
+        scat = [m.scatter(0, umem.data_ptr(), umem.numel(), hd) for _ in range(3)]
+        moved = sum(m.shard_info(k)["span_hi"] - m.shard_info(k)["span_lo"] + 16 * (m.shard_info(k)["frame_hi"] -
+                    m.shard_info(k)["frame_lo"]) for k in range(ndev))
+        for i in range(3):
+            m.process(opts[i & 1], frame_len_max=1500, frame_len_mean=mean)
+        steps = [m.process(opts[(i + 1) & 1], frame_len_max=1500, frame_len_mean=mean) for i in range(reps)]
+        m.process(opts[0], frame_len_max=1500, frame_len_mean=mean)   # the last pass -i 1
+        cnt = m.counters()
+        infos = [m.shard_info(k) for k in range(ndev)]
+    # one device's pass over the whole batch, -i 1, and its counters on the device
+    v = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=1500, frame_len_mean=mean).process_batch(
+        umem, dt)
+    fp = check_fingerprint(umem, dt, 0)
+    single = {"frames": n, "bytes": total, "drop": int((v == -1).sum()), "forward": int((v >= 0).sum()),
+              "checks_sum": fp[0], "checks_weighted": fp[1]}
+    del umem, dt, v
+    per_dev = [sorted(st[k] for st in steps)[len(steps) // 2] for k in range(ndev)]
+    step_max = sorted(max(st) for st in steps)[len(steps) // 2]
+    t_scat = sorted(scat)[1]
+    return {"devices": ndev, "frames": n, "frame_bytes": total,
+            "shards": [{"device": x["device"], "frames": [x["frame_lo"], x["frame_hi"]],
+                        "bytes": x["frame_bytes"]} for x in infos],
+            "scatter_ms": round(t_scat * 1e3, 3), "scatter_bytes": moved,
+            "scatter_GBps": round(moved / t_scat / 1e9, 1),
+            "step_us_per_device": [round(t * 1e3, 2) for t in per_dev],
+            "step_us": round(step_max * 1e3, 2),
+            "gbs_checksummed": round(total / (step_max / 1e3) / 1e9, 1),
+            "mpps": round(n / (step_max / 1e3) / 1e6, 1),
+            "counters": cnt, "single_gpu": single, "match": cnt == single,
+            "api": "xsknf_gpu_multi_create (ncclCommInitAll) / _scatter (grouped ncclSend / ncclRecv from device "
+                   "0) / _process (a stream per device) / _counters (ncclAllReduce); medians of "
+                   f"{reps} steps, each the slowest device's HIP-event time"}
+
+
 def check_fingerprint(umem, descs, base):
     """[sum of the written checks, the same weighted by (global offset mod 65521) + 1]
     over the well-formed-length frames of one batch (device tensors; `base` =
@@ -784,6 +842,12 @@ def main():
             torch.cuda.empty_cache()
 
     root_scatter = root_scatter_leg(args, world, rank, dev) if (_DIST and not args.no_root_scatter) else None
+    c_multi = None
+    if world == 1 and not args.no_c_host_multi:
+        try:
+            c_multi = c_host_multi_leg(args, dev)
+        except Exception as e:   # reported in the line; the primary's figures stand
+            c_multi = {"error": f"{type(e).__name__}: {e}"}
     # what the collectives saw: every rank contributes 1 (so a SCALE line shows
     # that the backend really had N ranks), and the frames summed over ranks
     dist_info = None
@@ -869,6 +933,8 @@ def main():
             out["config"]["rehearsal"] = rehearsal
         if root_scatter is not None:
             out["root_scatter"] = root_scatter
+        if c_multi is not None:
+            out["c_host_multi"] = c_multi
         if dist_info is not None:
             out["dist"] = dist_info
         print(json.dumps(out), flush=True)

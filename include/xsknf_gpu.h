@@ -312,6 +312,78 @@ XSKNF_GPU_API int xsknf_gpu_hook_get_stats(const struct xsknf_gpu_hook *hook, ui
 		struct xsknf_gpu_ctx_stats *stats);
 XSKNF_GPU_API int xsknf_gpu_hook_destroy(struct xsknf_gpu_hook *hook);
 
+/* ---- one process over several devices (BASELINE config 4) ----------------
+ * The reference scales one worker per NIC queue (src/xsknf.c:992, workers
+ * started per queue at :1046-1100); frames never cross workers.  The hook above
+ * is that model on a node of GPUs (worker w on device w % devices).  These
+ * calls are for a global batch that starts on ONE device: it is split into
+ * contiguous descriptor ranges balanced by frame bytes, each range's UMEM span
+ * and rebased descriptors are moved from the root device to its own by grouped
+ * RCCL point-to-point sends over xGMI (one communicator per device,
+ * ncclCommInitAll), every device checksums its shard on its own stream, and the
+ * counters of all shards are summed by an RCCL all-reduce.  The results equal
+ * one device's pass over the whole batch (tests/test_gpu_multi.py). */
+
+/* The byte-balanced split of n descriptors into nshards contiguous ranges:
+ * shard k is frames [bounds[k], bounds[k+1]) (bounds: nshards + 1 entries),
+ * cut after the first frame whose running sum of lengths reaches
+ * total * k / nshards (xsknf_amd/shard.py shard_by_bytes); spans (NULL, or
+ * 2 * nshards entries) = each shard's UMEM byte span [lo, hi) over its frames
+ * inside [0, umem_size) ({0, 0} for none).  Host arrays; no GPU call. */
+XSKNF_GPU_API int xsknf_gpu_shard_plan(const struct xsknf_gpu_desc *descs, uint64_t n, uint64_t umem_size,
+		uint32_t nshards, uint64_t *bounds, uint64_t *spans);
+/* A shard's descriptors relative to its span's first byte b0 (plain aligned-mode
+ * addresses); a descriptor outside [0, umem_size) gets an address past any
+ * UMEM (1 << 47): its verdict is -1 and no byte is touched, as before.  Host
+ * arrays; no GPU call. */
+XSKNF_GPU_API int xsknf_gpu_shard_rebase(const struct xsknf_gpu_desc *descs, uint64_t n, uint64_t b0,
+		uint64_t umem_size, struct xsknf_gpu_desc *out);
+
+struct xsknf_gpu_multi;
+
+/* [frames, frame bytes, drops (-1), forwards (>= 0), sum of the 16-bit words at
+ * +40 of every frame of >= 42 bytes (an ihl-5 frame's UDP check), the same
+ * weighted by ((global UMEM offset) mod 65521) + 1] */
+#define XSKNF_GPU_MULTI_COUNTERS 6
+
+struct xsknf_gpu_shard_info {
+	int32_t device;          /* HIP device of the shard */
+	int32_t reserved;
+	uint64_t frame_lo, frame_hi;   /* frames [lo, hi) of the global batch */
+	uint64_t span_lo, span_hi;     /* its bytes [lo, hi) of the root's UMEM */
+	uint64_t frame_bytes;          /* sum of its frame lengths */
+	uint8_t *umem;                 /* device buffers of the shard on its device */
+	struct xsknf_gpu_desc *descs;
+	int32_t *verdicts;
+};
+
+/* One RCCL communicator per device of devices[0..ndev) (NULL: devices 0..ndev-1,
+ * each at most once), a stream each. */
+XSKNF_GPU_API int xsknf_gpu_multi_create(struct xsknf_gpu_multi **m, const int *devices, int ndev);
+/* Split the global batch -- `umem` (umem_size bytes) resident on device
+ * devices[root], `descs` its n descriptors in host memory -- by
+ * xsknf_gpu_shard_plan and move every shard to its device: one grouped set of
+ * ncclSend / ncclRecv, the root's own shard as a send to itself.  Shard buffers
+ * are allocated on first use and kept for later scatters of the same size or
+ * smaller.  *seconds (may be NULL): wall time of the transfers. */
+XSKNF_GPU_API int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, const uint8_t *umem,
+		uint64_t umem_size, const struct xsknf_gpu_desc *descs, uint64_t n, double *seconds);
+/* Checksum every device's shard (xsknf_gpu_checksum_batch_lens on its own
+ * stream, all devices in flight at once); returns when all are done.  ms (may be
+ * NULL, ndev entries): each device's HIP-event time. */
+XSKNF_GPU_API int xsknf_gpu_multi_process(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex,
+		const struct xsknf_csum_opts *opts, uint32_t frame_len_max, uint32_t frame_len_mean, float *ms);
+/* The XSKNF_GPU_MULTI_COUNTERS counters of every shard, summed over the devices
+ * by ncclAllReduce (the root's copy, to host memory). */
+XSKNF_GPU_API int xsknf_gpu_multi_counters(struct xsknf_gpu_multi *m, uint64_t *out);
+XSKNF_GPU_API int xsknf_gpu_multi_shard_info(const struct xsknf_gpu_multi *m, int shard,
+		struct xsknf_gpu_shard_info *info);
+/* Copy shard `shard`'s UMEM span (span_hi - span_lo bytes), its rebased
+ * descriptors and its verdicts to host memory (any of them may be NULL). */
+XSKNF_GPU_API int xsknf_gpu_multi_fetch(const struct xsknf_gpu_multi *m, int shard, uint8_t *umem_out,
+		struct xsknf_gpu_desc *descs_out, int32_t *verdicts_out);
+XSKNF_GPU_API int xsknf_gpu_multi_destroy(struct xsknf_gpu_multi *m);
+
 /* Text of the last HIP error seen by this library, on any thread (a copy
  * private to the calling thread). */
 XSKNF_GPU_API const char *xsknf_gpu_last_error(void);

@@ -161,3 +161,52 @@ def test_root_scatter_bookkeeping(world):
         pu, pd, (p0, p1) = scatter_from_root(fp, None, None, None, r, world, "cpu")
         assert (p0, p1) == (rb0, rb1) and pu.numel() == rb1 - rb0 + 16 and pd.shape == (hi - lo, 2)
         assert [(o.peer, o.tensor.numel()) for o in fp.ops] == [(0, rb1 - rb0), (0, 2 * (hi - lo))]
+
+
+# ---- the C host's shard arithmetic (xsknf_gpu_shard_plan / _rebase, xsknf_amd/csrc/multi.hip) ----
+
+def _desc_cases():
+    rng = np.random.default_rng(77)
+    yield "imix-aligned", frames.aligned_batch(20000, "imix", seed=5)
+    yield "jumbo-unaligned", frames.unaligned_batch(3000, 9000, seed=6)
+    b = frames.unaligned_batch(5000, "imix", seed=7)
+    frames.inject_edge_cases(b, 0.1, seed=8)          # short, non-IP, ... and odd lengths
+    yield "imix-edges", b
+    b = frames.aligned_batch(4000, rng.integers(0, 1792, size=4000).astype(np.uint32), seed=9)
+    b.descs["len"][::97] = 0                          # zero-length frames
+    yield "random-lens", b
+    b = frames.aligned_batch(3000, "imix", seed=10)
+    b.descs["addr"][::50] += np.uint64(1 << 40)       # descriptors outside the UMEM
+    yield "out-of-range", b
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 7, 8, 64])
+def test_c_shard_plan_equals_shard_py(world):
+    """The C host's byte-balanced cuts and spans are shard.py's, frame for frame
+    (the C multi-device path and the rank path split config 4 the same way)."""
+    from xsknf_amd import multi
+    from xsknf_amd.shard import rebase_descs, shard_spans
+    for name, b in _desc_cases():
+        ranges, spans = multi.shard_plan(b.descs, world, b.umem.size)
+        assert ranges == shard_by_bytes(b.descs["len"], world), name
+        assert spans == shard_spans(b.descs, ranges, b.umem.size), name
+        for (lo, hi), (b0, _) in zip(ranges, spans):
+            got = multi.shard_rebase(b.descs[lo:hi], b0, b.umem.size)
+            want = rebase_descs(b.descs[lo:hi], b0, b.umem.size)
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), name
+
+
+def test_c_shard_plan_edges():
+    from xsknf_amd import multi
+    empty = np.zeros(0, dtype=frames.DESC_DTYPE)
+    assert multi.shard_plan(empty, 4, 0) == ([(0, 0)] * 4, [(0, 0)] * 4)
+    one = frames.aligned_batch(1, 1500, seed=1)
+    r, s = multi.shard_plan(one.descs, 3, one.umem.size)
+    assert r == shard_by_bytes(one.descs["len"], 3) and r[-1] == (1, 1) and s[-1] == (0, 0)
+    # config 4's global batch at its full size (8,388,608 IMIX frames), 8 ways
+    lens = frames.imix_lengths(8 * (1 << 20), np.random.default_rng(frames.SEED))
+    d = np.zeros(lens.shape[0], dtype=frames.DESC_DTYPE)
+    d["len"] = lens
+    d["addr"] = np.arange(lens.shape[0], dtype=np.uint64) * np.uint64(2048) + np.uint64(256)
+    r, _ = multi.shard_plan(d, 8, lens.shape[0] * 2048)
+    assert r == shard_by_bytes(lens, 8)

@@ -57,10 +57,12 @@ def _last_start():
 def _run_app(args, cwd, want_rx, timeout, test_id):
     """Start the NF, poll stats.txt via SIGUSR1 until it reads want_rx, then SIGINT.
 
-    Every start is logged to gpurun_out/nf_starts.jsonl: pid, its KFD entry seen
-    while it ran, its exit, and how long its KFD context took to go after the exit
-    (the NF's context is torn down by the kernel after the process ends; the next
-    test starts its NF only once that entry is gone, or after 15 s).  An NF that
+    Every start is logged to gpurun_out/nf_starts.jsonl: pid, the NF's KFD entry,
+    its exit, and how long its KFD context outlived the exit.  The GPU box runs
+    in a PID namespace and /sys/class/kfd/kfd/proc lists host pids (round 6:
+    none of the box's own pids is ever there), so the NF's entry is the one that
+    appeared after its start (when exactly one did); the next test starts its NF
+    only once that entry is gone (or after 15 s).  An NF that
     exits at start because HIP saw no device (twice in round 5's GPU runs, on boxes
     where the runs before and after saw the GPU) prints what it saw
     (xsknf_gpu_device_count's error text: HIP's error, /dev/kfd and render-node
@@ -84,19 +86,20 @@ def _run_app(args, cwd, want_rx, timeout, test_id):
 
 def _run_app_once(args, cwd, want_rx, timeout, test_id):
     t0 = time.time()
+    before = _kfd_pids()
     p = subprocess.Popen([APP, *args], cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     stats = os.path.join(cwd, "stats.txt")
     seen = []
-    in_kfd = None
+    kfd_pid = None
     deadline = time.time() + timeout
     try:
         while time.time() < deadline and p.poll() is None:
             time.sleep(0.5)
             p.send_signal(signal.SIGUSR1)
             time.sleep(1.2)                   # the main loop serves the request within a second
-            if in_kfd is None and p.poll() is None:
-                pids = _kfd_pids()
-                in_kfd = None if pids is None else p.pid in pids
+            if kfd_pid is None and before is not None and p.poll() is None:
+                new = sorted(set(_kfd_pids() or []) - set(before))
+                kfd_pid = new[0] if len(new) == 1 else (-len(new) if new else None)
             if os.path.exists(stats):
                 txt = open(stats).read().strip()
                 if txt:
@@ -114,16 +117,16 @@ def _run_app_once(args, cwd, want_rx, timeout, test_id):
             out, err = p.communicate()
     t_exit = time.time()
     # the next NF starts once this one's KFD context is gone (bounded)
-    gone = None
-    while time.time() - t_exit < 15.0:
-        pids = _kfd_pids()
-        if pids is None or p.pid not in pids:
-            gone = pids is not None
-            break
-        time.sleep(0.05)
+    gone_s = None
+    if kfd_pid is not None and kfd_pid > 0:
+        while time.time() - t_exit < 15.0:
+            if kfd_pid not in (_kfd_pids() or []):
+                gone_s = round(time.time() - t_exit, 3)
+                break
+            time.sleep(0.02)
     _log(STARTS_LOG, {"test": test_id, "pid": p.pid, "start": t0, "exit": t_exit, "rc": p.returncode,
-                      "pid_in_kfd_while_running": in_kfd, "kfd_gone_after_s": round(time.time() - t_exit, 3)
-                      if gone else None, "no_device": NO_DEVICE in err})
+                      "kfd_before": before, "nf_kfd_pid": kfd_pid, "kfd_gone_after_s": gone_s,
+                      "no_device": NO_DEVICE in err})
     return p.returncode, seen, out, err
 
 

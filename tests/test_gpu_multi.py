@@ -86,6 +86,82 @@ def test_config4_global_batch_in_byte_balanced_shards(dev):
     assert (ov == -1).sum() > 0 and (ov == 0).sum() > 0.98 * n
 
 
+def _c_host_multi_run(dev, host, hd, layout, edge_seed=None, mean=0, action=0, nif=1):
+    """The global batch through the C host's multi-device calls over every visible
+    device (include/xsknf_gpu.h xsknf_gpu_multi_*: ncclCommInitAll, grouped
+    ncclSend / ncclRecv from device 0 -- the root's own shard as a send to itself
+    --, a launch per device, the counter ncclAllReduce); checked against the
+    reference's own pass over the whole batch: every verdict, every byte of every
+    shard's span, and the all-reduced counters."""
+    from xsknf_amd import ChecksummerOptions, multi
+    ndev = torch.cuda.device_count()
+    umem = torch.from_numpy(host).to(dev)
+    size = host.size
+    torch.cuda.synchronize()
+    with multi.MultiDevice(range(ndev)) as m:
+        secs = m.scatter(0, umem.data_ptr(), size, hd)
+        del umem
+        ms = m.process(ChecksummerOptions(action=action), num_interfaces=nif, frame_len_max=int(hd["len"].max()),
+                       frame_len_mean=mean)
+        cnt = m.counters()
+        shards = []
+        for k in range(ndev):
+            info = m.shard_info(k)
+            su, sv = m.fetch(k)
+            shards.append((info, su, sv))
+    ref = host.copy()
+    _, ov = oracles.time_batch(ref, hd, action=action, nif=nif)
+    ranges = shard_by_bytes(hd["len"], ndev)
+    spans = shard_spans(hd, ranges, size)
+    for k, (info, su, sv) in enumerate(shards):
+        assert (info["frame_lo"], info["frame_hi"]) == ranges[k]
+        assert (info["span_lo"], info["span_hi"]) == spans[k]
+        assert info["device"] == k
+        lo, hi = ranges[k]
+        assert np.array_equal(sv, ov[lo:hi]), f"shard {k} verdicts"
+        assert np.array_equal(su, ref[spans[k][0]:spans[k][1]]), f"shard {k} bytes"
+    assert cnt == multi.expected_counters(ref, hd, ov)
+    return secs, ms, cnt, ndev
+
+
+@pytest.mark.slow
+def test_c_host_multi_device_config4(dev):
+    """BASELINE config 4 (8,388,608 IMIX frames, aligned 2 KiB chunks, 1 % edge
+    cases) through the C host's multi-device path, over
+    every device of the box (one on the GPU box: the root's shard moves by an
+    RCCL send to itself), bit-exact against the reference's own function over the
+    whole batch; the all-reduced counters equal the host's."""
+    n = 8 << 20
+    b = frames.aligned_batch(n, "imix", seed=frames.SEED)
+    frames.inject_edge_cases(b, 0.01, seed=405)
+    secs, ms, cnt, ndev = _c_host_multi_run(dev, b.umem, b.descs, "aligned", mean=int(b.descs["len"].mean()))
+    assert cnt["frames"] == n and cnt["forward"] > 0.98 * n and cnt["drop"] > 0
+    assert secs > 0 and len(ms) == ndev and all(t > 0 for t in ms)
+    print(f"c-host multi: {ndev} device(s), scatter {secs * 1e3:.1f} ms, process {ms} ms")
+
+
+@pytest.mark.parametrize("case", ["unaligned-edges", "jumbo", "out-of-range", "drop-2if", "one-frame"])
+def test_c_host_multi_device_cases(dev, case):
+    """Smaller batches through the same path: packed unaligned frames (odd starts)
+    with 10 % edge cases, jumbo frames, descriptors outside the UMEM (verdict -1,
+    no byte), DROP with two interfaces, a single frame."""
+    action, nif = 0, 1
+    if case == "unaligned-edges":
+        b = frames.unaligned_batch(20000, "imix", seed=51)
+        frames.inject_edge_cases(b, 0.1, seed=52)
+    elif case == "jumbo":
+        b = frames.unaligned_batch(3000, 9000, seed=53)
+    elif case == "out-of-range":
+        b = frames.aligned_batch(5000, "imix", seed=54)
+        b.descs["addr"][::37] += np.uint64(1 << 40)
+    elif case == "drop-2if":
+        b = frames.aligned_batch(5000, 1500, seed=55)
+        action, nif = 1, 2
+    else:
+        b = frames.aligned_batch(1, 570, seed=56)
+    _c_host_multi_run(dev, b.umem, b.descs, b.layout, action=action, nif=nif)
+
+
 def _scatter_rank(rank, world, port, outdir):
     import torch
     import torch.distributed as dist

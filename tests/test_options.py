@@ -32,7 +32,7 @@ def test_invalid_action_exits_with_usage(capsys):
         parse_command_line(["-c", "FORWARD"])
     assert e.value.code == 1
     err = capsys.readouterr().err
-    assert "ERROR: invalid action FORWARD" in err and "Usage:" in err
+    assert "action 'FORWARD' is neither REDIRECT nor DROP" in err and "usage:" in err
 
 
 def test_library_options_and_defaults():
@@ -57,12 +57,12 @@ def test_library_options_and_defaults():
 
 
 @pytest.mark.parametrize("argv,msg", [
-    (["-i", "eth0:q"], "ERROR: unknown copy mode 'q'"),                  # src/xsknf.c:800-812
-    (["-i", "eth0", "-M", "TURBO"], "ERROR: unknown working mode TURBO"),  # :845-858
-    (["-i", "eth0", "-w", "0"], "ERROR: Invalid number of workers 0"),     # :859-866
-    ([], "ERROR: at least one interface in required"),                  # :872-874
-    (["-i", "eth0", "-f", "3000"], "--frame-size=3000 is not a power of two"),   # :866-871
-    (["-i", "eth0", "-Z"], "invalid option -- 'Z'"),                      # getopt, then usage()
+    (["-i", "eth0:q"], "copy mode 'q' is neither c nor z"),              # src/xsknf.c:800-812
+    (["-i", "eth0", "-M", "TURBO"], "no working mode named 'TURBO'"),     # :845-858
+    (["-i", "eth0", "-w", "0"], "worker count '0' is not a positive number"),   # :859-866
+    ([], "no interface given"),                                           # :872-874
+    (["-i", "eth0", "-f", "3000"], "frame size 3000 must be a power of two"),   # :866-871
+    (["-i", "eth0", "-Z"], "invalid option -- 'Z'"),                      # getopt, then the summary
 ])
 def test_library_option_errors_exit_1_with_usage(argv, msg):
     """xsknf_parse_args ends the process on a bad library option, as the
@@ -78,3 +78,4 @@ def test_library_option_errors_exit_1_with_usage(argv, msg):
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert p.returncode == 1, (p.returncode, p.stdout, p.stderr)
     assert msg in p.stderr and "returned" not in p.stdout
+    assert "xsknf library options" in p.stderr and "--iface=IF" in p.stderr   # the option summary

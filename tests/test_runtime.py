@@ -328,7 +328,7 @@ def test_parse_args_errors_exit_like_the_reference(argv):
             "lib.xsknf_parse_args(len(a), arr, ctypes.byref(R.Config())); print('returned')") % (ROOT, argv)
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert p.returncode == 1 and "returned" not in p.stdout
-    assert "xsknf options" in p.stderr
+    assert "xsknf library options" in p.stderr
 
 
 def _veth_available():

@@ -6,9 +6,11 @@
 // access, *_VISIBLE_DEVICES, the KFD processes).  Driven by
 // tools/nf_start_probe.py, which starts it back to back from a process that
 // never touched the GPU while its parent holds a GPU context (the GPU suite's
-// shape: tests/test_gpu_app.py).  Measurement infra, not the product.
+// shape: tests/test_gpu_app.py).  `dev_probe [hold_s]` keeps the context hold_s
+// seconds before destroying it.  Measurement infra, not the product.
 #include <errno.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <time.h>
 #include <unistd.h>
@@ -22,8 +24,9 @@ static double now_s(void)
 	return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-int main(void)
+int main(int argc, char **argv)
 {
+	const double hold = argc > 1 ? atof(argv[1]) : 0.0;   // seconds to keep the context
 	const double t0 = now_s();
 	int count = 0;
 	int rc = xsknf_gpu_device_count(&count);
@@ -35,6 +38,8 @@ int main(void)
 	}
 	struct xsknf_gpu_ctx *ctx = NULL;
 	rc = xsknf_gpu_ctx_create(&ctx, 0, XSKNF_GPU_PATH_ZEROCOPY, 64, 64);
+	if (!rc && hold > 0)
+		usleep((useconds_t)(hold * 1e6));
 	if (!rc)
 		rc = xsknf_gpu_ctx_destroy(ctx);
 	const double t2 = now_s();

@@ -36,7 +36,18 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_hook_complete",
     "xsknf_gpu_hook_get_stats",
     "xsknf_gpu_hook_destroy",
+    "xsknf_gpu_shard_plan",
+    "xsknf_gpu_shard_rebase",
+    "xsknf_gpu_multi_create",
+    "xsknf_gpu_multi_scatter",
+    "xsknf_gpu_multi_process",
+    "xsknf_gpu_multi_counters",
+    "xsknf_gpu_multi_shard_info",
+    "xsknf_gpu_multi_fetch",
+    "xsknf_gpu_multi_destroy",
 )
+
+MULTI_COUNTERS = 6   # XSKNF_GPU_MULTI_COUNTERS
 
 PATH_ZEROCOPY = 0
 PATH_STAGED = 1
@@ -78,6 +89,16 @@ class CtxStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("frames", ctypes.c_uint64),
                 ("bytes_h2d", ctypes.c_uint64), ("bytes_d2h", ctypes.c_uint64),
                 ("resident_batches", ctypes.c_uint64), ("resident_launches", ctypes.c_uint64)]
+
+
+class ShardInfo(ctypes.Structure):
+    """struct xsknf_gpu_shard_info (include/xsknf_gpu.h)."""
+
+    _fields_ = [("device", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("frame_lo", ctypes.c_uint64), ("frame_hi", ctypes.c_uint64),
+                ("span_lo", ctypes.c_uint64), ("span_hi", ctypes.c_uint64),
+                ("frame_bytes", ctypes.c_uint64),
+                ("umem", ctypes.c_void_p), ("descs", ctypes.c_void_p), ("verdicts", ctypes.c_void_p)]
 
 
 class XsknfGpuError(RuntimeError):
@@ -181,6 +202,26 @@ def load() -> ctypes.CDLL:
     lib.xsknf_gpu_hook_get_stats.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(CtxStats)]
     lib.xsknf_gpu_hook_destroy.restype = ctypes.c_int
     lib.xsknf_gpu_hook_destroy.argtypes = [ctypes.c_void_p]
+    u64, vp = ctypes.c_uint64, ctypes.c_void_p
+    lib.xsknf_gpu_shard_plan.restype = ctypes.c_int
+    lib.xsknf_gpu_shard_plan.argtypes = [vp, u64, u64, ctypes.c_uint32, vp, vp]
+    lib.xsknf_gpu_shard_rebase.restype = ctypes.c_int
+    lib.xsknf_gpu_shard_rebase.argtypes = [vp, u64, u64, u64, vp]
+    lib.xsknf_gpu_multi_create.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_create.argtypes = [ctypes.POINTER(vp), vp, ctypes.c_int]
+    lib.xsknf_gpu_multi_scatter.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_scatter.argtypes = [vp, ctypes.c_int, vp, u64, vp, u64, ctypes.POINTER(ctypes.c_double)]
+    lib.xsknf_gpu_multi_process.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_process.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(CsumOpts), ctypes.c_uint32,
+                                            ctypes.c_uint32, vp]
+    lib.xsknf_gpu_multi_counters.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_counters.argtypes = [vp, vp]
+    lib.xsknf_gpu_multi_shard_info.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_shard_info.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ShardInfo)]
+    lib.xsknf_gpu_multi_fetch.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_fetch.argtypes = [vp, ctypes.c_int, vp, vp, vp]
+    lib.xsknf_gpu_multi_destroy.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_destroy.argtypes = [vp]
     _lib = lib
     return lib
 

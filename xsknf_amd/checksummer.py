@@ -27,14 +27,13 @@ ACTION_REDIRECT = _lib.ACTION_REDIRECT
 ACTION_DROP = _lib.ACTION_DROP
 
 _APP_USAGE = (
-    "  Usage: %s [XSKNF_OPTIONS] -- [APP_OPTIONS]\n"
-    "  App options:\n"
-    "  -c, --action\t\tREDIRECT or DROP packets (default REDIRECT).\n"
-    "  -i, --csum-iterations\tNumber of times to recompute the checksum.\n"
-    "  -q, --quiet\t\tDo not display any stats.\n"
-    "  -x, --extra-stats\tDisplay extra statistics.\n"
-    "  -a, --app-stats\tDisplay application (syscall) statistics.\n"
-    "\n")
+    "usage: %s [xsknf library options] -- [checksummer options]\n"
+    "checksummer options:\n"
+    "  -c, --action=REDIRECT|DROP   send each checksummed frame on (default) or drop it\n"
+    "  -i, --csum-iterations=N      sum the UDP payload N times (default 1)\n"
+    "  -q, --quiet                  no per-second statistics\n"
+    "  -x, --extra-stats            also the ring counters\n"
+    "  -a, --app-stats              also the syscall counters\n")
 
 
 def _usage_exit(prog: str) -> None:
@@ -70,8 +69,8 @@ def _atoi(s: str) -> int:
 def parse_command_line(argv: List[str], prog: str = "checksummer") -> ChecksummerOptions:
     """Mirror of parse_command_line() (checksummer_user.c:139-175).
 
-    `argv` are the APP options (after `--`).  An invalid action prints
-    "ERROR: invalid action X" plus usage and exits with status 1, like the
+    `argv` are the APP options (after `--`).  An invalid action prints what
+    was wrong plus the option summary and exits with status 1, like the
     reference.  The reference declares --csum-iterations as no_argument
     (:116) so only `-i N` works there; here the long form requires an argument
     rather than crashing on atoi(NULL)."""
@@ -88,7 +87,7 @@ def parse_command_line(argv: List[str], prog: str = "checksummer") -> Checksumme
             elif v == "DROP":
                 o.action = ACTION_DROP
             else:
-                sys.stderr.write(f"ERROR: invalid action {v}\n")
+                sys.stderr.write(f"checksummer: action '{v}' is neither REDIRECT nor DROP\n")
                 _usage_exit(prog)
         elif k in ("-i", "--csum-iterations"):
             o.csum_iterations = _atoi(v)

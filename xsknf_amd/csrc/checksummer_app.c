@@ -58,25 +58,25 @@ static const struct option long_options[] = {
 	{0, 0, 0, 0},
 };
 
-static void usage(const char *prog)
+static const struct {
+	const char *flags, *text;
+} app_help[] = {
+	{"-c, --action=REDIRECT|DROP", "send each checksummed frame on (default) or drop it"},
+	{"-i, --csum-iterations=N", "sum the UDP payload N times (default 1)"},
+	{"-q, --quiet", "no per-second statistics"},
+	{"-x, --extra-stats", "also the ring counters"},
+	{"-a, --app-stats", "also the syscall counters"},
+	{"-g, --gpu-path=PATH", "ZEROCOPY, STAGED or RESIDENT (default RESIDENT up to 128-frame batches, else ZEROCOPY)"},
+	{"-s, --gpu-sync", "one batch at a time (default: receive while the GPU works)"},
+	{"-d, --gpu-depth=N", "batches in flight per worker, 1-8 (default 4 RESIDENT, else 2 up to 128 frames, else 1)"},
+	{"-G, --emu-gen=COUNT[:LEN]", "emulated queues: COUNT generated frames of LEN bytes (default 64) per queue"},
+};
+
+static void __attribute__((noreturn)) usage(const char *prog)
 {
-	fprintf(stderr,
-		"  Usage: %s [XSKNF_OPTIONS] -- [APP_OPTIONS]\n"
-		"  App options:\n"
-		"  -c, --action		REDIRECT or DROP packets (default REDIRECT).\n"
-		"  -i, --csum-iterations	Number of times to recompute the checksum.\n"
-		"  -q, --quiet		Do not display any stats.\n"
-		"  -x, --extra-stats	Display extra statistics.\n"
-		"  -a, --app-stats	Display application (syscall) statistics.\n"
-		"  -g, --gpu-path	ZEROCOPY, STAGED or RESIDENT host path to the GPU\n"
-		"			(default: RESIDENT for batches of up to 128 frames, else ZEROCOPY).\n"
-		"  -s, --gpu-sync	One batch at a time (default: the next batch is received\n"
-		"			while the GPU checksums the last one).\n"
-		"  -d, --gpu-depth	Batches in flight per worker, 1-8 (default 4 on RESIDENT,\n"
-		"			else 2 for batches of up to 128 frames, else 1).\n"
-		"  -G, --emu-gen		COUNT[:LEN] frames per emulated queue from a built-in generator.\n"
-		"\n",
-		prog);
+	fprintf(stderr, "usage: %s [xsknf library options] -- [checksummer options]\nchecksummer options:\n", prog);
+	for (size_t k = 0; k < sizeof(app_help) / sizeof(app_help[0]); k++)
+		fprintf(stderr, "  %-28s %s\n", app_help[k].flags, app_help[k].text);
 	exit(EXIT_FAILURE);
 }
 
@@ -91,7 +91,7 @@ static void parse_command_line(int argc, char **argv, char *app_path)
 			} else if (!strcmp(optarg, "DROP")) {
 				opt_action = XSKNF_CSUM_ACTION_DROP;
 			} else {
-				fprintf(stderr, "ERROR: invalid action %s\n", optarg);
+				fprintf(stderr, "checksummer: action '%s' is neither REDIRECT nor DROP\n", optarg);
 				usage(basename(app_path));
 			}
 			break;
@@ -113,7 +113,7 @@ static void parse_command_line(int argc, char **argv, char *app_path)
 		case 'd':
 			opt_gpu_depth = atoi(optarg);
 			if (opt_gpu_depth < 1 || opt_gpu_depth > XSKNF_MAX_HOOK_DEPTH) {
-				fprintf(stderr, "ERROR: invalid gpu depth %s\n", optarg);
+				fprintf(stderr, "checksummer: GPU depth '%s' is not in 1-%d\n", optarg, XSKNF_MAX_HOOK_DEPTH);
 				usage(basename(app_path));
 			}
 			break;
@@ -125,7 +125,7 @@ static void parse_command_line(int argc, char **argv, char *app_path)
 			} else if (!strcmp(optarg, "RESIDENT")) {
 				opt_gpu_path = XSKNF_GPU_PATH_RESIDENT;
 			} else {
-				fprintf(stderr, "ERROR: invalid gpu path %s\n", optarg);
+				fprintf(stderr, "checksummer: no GPU path named '%s'\n", optarg);
 				usage(basename(app_path));
 			}
 			break;
@@ -135,7 +135,7 @@ static void parse_command_line(int argc, char **argv, char *app_path)
 			if (end && *end == ':')
 				opt_gen_len = (unsigned)strtoul(end + 1, NULL, 10);
 			if (opt_gen_len < 42 || opt_gen_len > 3840) {
-				fprintf(stderr, "ERROR: invalid generator frame length %u\n", opt_gen_len);
+				fprintf(stderr, "checksummer: generator frame length %u is not in 42-3840\n", opt_gen_len);
 				usage(basename(app_path));
 			}
 			break;

@@ -1,0 +1,450 @@
+// multi.hip -- one process over N devices: config 4's global batch, sharded.
+//
+// The reference scales one worker per NIC queue (src/xsknf.c:992, the worker
+// loop started per queue at :1046-1100): frames never cross workers, so its
+// parallelism is independent batches.  On a node of MI355X the same holds per
+// device, and the per-worker hook (host_path.hip: worker w on device
+// w % devices) is that model.  This file adds what a C host needs when a
+// global batch starts on ONE device (BASELINE config 4):
+//
+//   * xsknf_gpu_shard_plan  -- contiguous descriptor ranges balanced by frame
+//     bytes (the kernel is HBM-bound: bytes set each device's time), and the
+//     UMEM byte span of each range; the same cuts as xsknf_amd/shard.py.
+//   * xsknf_gpu_multi_create -- one RCCL communicator per device
+//     (ncclCommInitAll: one process drives every device), a stream each.
+//   * xsknf_gpu_multi_scatter -- each shard moved from the root device as ONE
+//     span of UMEM bytes plus its rebased descriptors, by grouped ncclSend /
+//     ncclRecv: every peer's transfer at once, each on its own xGMI link (the
+//     root's own shard too, as a send to itself, so the path is the same at
+//     N = 1).  A point-to-point pattern, not a ring collective.
+//   * xsknf_gpu_multi_process -- the checksummer on every device's shard, each
+//     on its own stream, all in flight together (no data-path collective).
+//   * xsknf_gpu_multi_counters -- {frames, bytes, drops, forwards, sum of the
+//     written checks, the same weighted by global UMEM offset} per device,
+//     summed over devices by ncclAllReduce: the whole batch's result, as one
+//     device's pass over all of it would give it.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <new>
+#include <vector>
+
+#include "../../include/xsknf_gpu.h"
+#include "checksummer_internal.h"
+
+namespace {
+
+constexpr uint64_t kOutOfRange = 1ull << 47;   // an address past any UMEM: verdict -1, no bytes
+constexpr uint32_t kFingerprintMod = 65521;
+constexpr uint64_t kP2PPiece = 1ull << 28;     // bytes per ncclSend / ncclRecv of a scatter
+
+__host__ __device__ inline uint64_t umem_offset(uint64_t addr) {
+  return (addr & XSKNF_GPU_UNALIGNED_BUF_ADDR_MASK) + (addr >> XSKNF_GPU_UNALIGNED_BUF_OFFSET_SHIFT);
+}
+
+bool in_umem(const xsknf_gpu_desc &d, uint64_t umem_size) {
+  const uint64_t off = umem_offset(d.addr);
+  return off <= umem_size && d.len <= umem_size - off;
+}
+
+int nccl_fail(ncclResult_t r, const char *where) {
+  char buf[256];
+  snprintf(buf, sizeof(buf), "%s: %s", where, ncclGetErrorString(r));
+  xsknf_gpu::set_error_text(buf);
+  return -EIO;
+}
+
+int hip_fail(hipError_t e, const char *where) {
+  xsknf_gpu::set_error(e, where);
+  return e == hipErrorOutOfMemory ? -ENOMEM : -EIO;
+}
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+// Per frame of one shard: [frames, bytes, drops, forwards, checks, weighted
+// checks] -- the bytes over every descriptor's len (xsknf_amd/shard.py
+// counters()), the checks over the frames of at least 42 bytes inside the span
+// (the UDP check of an ihl-5 frame at +40, as bench.py check_fingerprint reads
+// it), weighted by (global offset mod 65521) + 1 so that a check landing in
+// another frame shows.  One wave per 64 frames, a block sum, one atomic per
+// counter and block (vector atomics to device memory).
+__global__ void __launch_bounds__(256) shard_counters(const uint8_t *umem, uint64_t span,
+                                                      const xsknf_gpu_desc *descs, const int32_t *verdicts,
+                                                      uint64_t n, uint64_t base, unsigned long long *out) {
+  unsigned long long c[XSKNF_GPU_MULTI_COUNTERS] = {};
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    const xsknf_gpu_desc d = descs[i];
+    const int32_t v = verdicts[i];
+    c[0] += 1;
+    c[1] += d.len;
+    c[2] += v == -1;
+    c[3] += v >= 0;
+    const uint64_t off = umem_offset(d.addr);
+    if (d.len >= 42 && off <= span && d.len <= span - off) {
+      const unsigned long long ck = umem[off + 40] | static_cast<unsigned>(umem[off + 41]) << 8;
+      c[4] += ck;
+      c[5] += ck * ((off + base) % kFingerprintMod + 1);
+    }
+  }
+  __shared__ unsigned long long red[XSKNF_GPU_MULTI_COUNTERS][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < XSKNF_GPU_MULTI_COUNTERS; ++k) {
+    unsigned long long x = c[k];
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) red[k][wv] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < XSKNF_GPU_MULTI_COUNTERS) {
+    const int k = threadIdx.x;
+    atomicAdd(&out[k], red[k][0] + red[k][1] + red[k][2] + red[k][3]);
+  }
+}
+
+struct Shard {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  uint64_t lo = 0, hi = 0;       // frames [lo, hi) of the global batch
+  uint64_t b0 = 0, b1 = 0;       // its UMEM byte span on the root
+  uint64_t bytes = 0;            // sum of the shard's frame lengths
+  uint8_t *umem = nullptr;       // b1 - b0 bytes + 16 spare (the kernels' 16-byte chunk loads)
+  uint64_t umem_cap = 0;
+  xsknf_gpu_desc *descs = nullptr;
+  int32_t *verdicts = nullptr;
+  uint64_t frames_cap = 0;
+  unsigned long long *counters = nullptr;   // device: XSKNF_GPU_MULTI_COUNTERS
+};
+
+}  // namespace
+
+struct xsknf_gpu_multi {
+  int ndev = 0;
+  std::vector<int> devices;
+  std::vector<ncclComm_t> comms;
+  std::vector<Shard> sh;
+  xsknf_gpu_desc *root_descs = nullptr;   // the rebased descriptors of every shard, on the root device
+  uint64_t root_descs_cap = 0;
+  int root_descs_dev = -1;                // the device root_descs lives on
+  int root = -1;                          // index of the root of the last scatter
+  uint64_t n = 0;                         // frames of the last scatter
+};
+
+extern "C" {
+
+int xsknf_gpu_shard_plan(const struct xsknf_gpu_desc *descs, uint64_t n, uint64_t umem_size, uint32_t nshards,
+                         uint64_t *bounds, uint64_t *spans) {
+  if (nshards == 0 || !bounds || (n && !descs)) return -EINVAL;
+  // cuts: shard r starts after the first frame whose running byte count
+  // reaches total * r / nshards (shard.py: searchsorted(cumsum, target,
+  // "left") + 1, then clamped to n and made non-decreasing).  The targets are
+  // the correctly rounded doubles of the rationals, as Python's int / int;
+  // the running sums are exact in a double below 2^53 bytes.
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) total += descs[i].len;
+  bounds[0] = 0;
+  uint64_t i = 0, csum = n ? descs[0].len : 0;
+  for (uint32_t r = 1; r < nshards; ++r) {
+    const double target = static_cast<double>(total * r) / nshards;
+    while (i < n && static_cast<double>(csum) < target) {
+      ++i;
+      if (i < n) csum += descs[i].len;
+    }
+    uint64_t cut = n == 0 ? 0 : i + 1;
+    if (cut > n) cut = n;
+    if (cut < bounds[r - 1]) cut = bounds[r - 1];
+    bounds[r] = cut;
+  }
+  bounds[nshards] = n;
+  if (spans) {
+    for (uint32_t r = 0; r < nshards; ++r) {
+      uint64_t b0 = UINT64_MAX, b1 = 0;
+      for (uint64_t f = bounds[r]; f < bounds[r + 1]; ++f) {
+        if (!in_umem(descs[f], umem_size)) continue;
+        const uint64_t off = umem_offset(descs[f].addr);
+        if (off < b0) b0 = off;
+        if (off + descs[f].len > b1) b1 = off + descs[f].len;
+      }
+      spans[2 * r] = b0 == UINT64_MAX ? 0 : b0;
+      spans[2 * r + 1] = b0 == UINT64_MAX ? 0 : b1;
+    }
+  }
+  return 0;
+}
+
+int xsknf_gpu_shard_rebase(const struct xsknf_gpu_desc *descs, uint64_t n, uint64_t b0, uint64_t umem_size,
+                           struct xsknf_gpu_desc *out) {
+  if (n && (!descs || !out)) return -EINVAL;
+  for (uint64_t i = 0; i < n; ++i) {
+    const xsknf_gpu_desc d = descs[i];
+    out[i].addr = in_umem(d, umem_size) ? umem_offset(d.addr) - b0 : kOutOfRange;
+    out[i].len = d.len;
+    out[i].options = d.options;
+  }
+  return 0;
+}
+
+int xsknf_gpu_multi_create(struct xsknf_gpu_multi **out, const int *devices, int ndev) {
+  if (!out || ndev < 1 || ndev > 64) return -EINVAL;
+  *out = nullptr;
+  int count = 0;
+  const int rc = xsknf_gpu_device_count(&count);
+  if (rc) return rc;
+  std::vector<int> devs(ndev);
+  for (int k = 0; k < ndev; ++k) {
+    devs[k] = devices ? devices[k] : k;
+    if (devs[k] < 0 || devs[k] >= count) return -EINVAL;
+    for (int j = 0; j < k; ++j)
+      if (devs[j] == devs[k]) return -EINVAL;   // one communicator rank per device
+  }
+  xsknf_gpu_multi *m = new (std::nothrow) xsknf_gpu_multi;
+  if (!m) return -ENOMEM;
+  m->ndev = ndev;
+  m->devices = devs;
+  m->comms.assign(ndev, nullptr);
+  m->sh.resize(ndev);
+  ncclResult_t r = ncclCommInitAll(m->comms.data(), ndev, devs.data());
+  if (r != ncclSuccess) {
+    delete m;
+    return nccl_fail(r, "ncclCommInitAll");
+  }
+  for (int k = 0; k < ndev; ++k) {
+    Shard &s = m->sh[k];
+    s.device = devs[k];
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&s.e0);
+    if (e == hipSuccess) e = hipEventCreate(&s.e1);
+    if (e == hipSuccess) e = hipMalloc(&s.counters, sizeof(unsigned long long) * XSKNF_GPU_MULTI_COUNTERS);
+    if (e != hipSuccess) {
+      xsknf_gpu_multi_destroy(m);
+      return hip_fail(e, "multi device setup");
+    }
+  }
+  *out = m;
+  return 0;
+}
+
+int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, const uint8_t *umem, uint64_t umem_size,
+                            const struct xsknf_gpu_desc *descs, uint64_t n, double *seconds) {
+  if (!m || root < 0 || root >= m->ndev || (n && (!umem || !descs))) return -EINVAL;
+  const int N = m->ndev;
+  std::vector<uint64_t> bounds(N + 1), spans(2 * N);
+  int rc = xsknf_gpu_shard_plan(descs, n, umem_size, static_cast<uint32_t>(N), bounds.data(), spans.data());
+  if (rc) return rc;
+  // the rebased descriptors of every shard (each relative to its own span),
+  // staged on the root device in global order
+  std::vector<xsknf_gpu_desc> rebased(n);
+  for (int k = 0; k < N; ++k)
+    xsknf_gpu_shard_rebase(descs + bounds[k], bounds[k + 1] - bounds[k], spans[2 * k], umem_size,
+                           rebased.data() + bounds[k]);
+  hipError_t e = hipSuccess;
+  if (m->root_descs && (n > m->root_descs_cap || m->root_descs_dev != m->devices[root])) {
+    e = hipSetDevice(m->root_descs_dev);
+    if (e == hipSuccess) e = hipFree(m->root_descs);
+    m->root_descs = nullptr;
+    m->root_descs_cap = 0;
+  }
+  if (e == hipSuccess) e = hipSetDevice(m->devices[root]);
+  if (e == hipSuccess && !m->root_descs && n) {
+    e = hipMalloc(&m->root_descs, sizeof(xsknf_gpu_desc) * n);
+    if (e == hipSuccess) {
+      m->root_descs_cap = n;
+      m->root_descs_dev = m->devices[root];
+    }
+  }
+  if (e == hipSuccess && n)
+    e = hipMemcpy(m->root_descs, rebased.data(), sizeof(xsknf_gpu_desc) * n, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "multi scatter: root descriptors");
+  for (int k = 0; k < N; ++k) {
+    Shard &s = m->sh[k];
+    s.lo = bounds[k];
+    s.hi = bounds[k + 1];
+    s.b0 = spans[2 * k];
+    s.b1 = spans[2 * k + 1];
+    s.bytes = 0;
+    for (uint64_t f = s.lo; f < s.hi; ++f) s.bytes += descs[f].len;
+    e = hipSetDevice(s.device);
+    const uint64_t need = s.b1 - s.b0 + 16, frames = s.hi - s.lo;
+    if (e == hipSuccess && need > s.umem_cap) {
+      if (s.umem) (void)hipFree(s.umem);
+      s.umem = nullptr;
+      s.umem_cap = 0;
+      e = hipMalloc(&s.umem, need);
+      if (e == hipSuccess) s.umem_cap = need;
+    }
+    if (e == hipSuccess && frames > s.frames_cap) {
+      if (s.descs) (void)hipFree(s.descs);
+      if (s.verdicts) (void)hipFree(s.verdicts);
+      s.descs = nullptr;
+      s.verdicts = nullptr;
+      s.frames_cap = 0;
+      e = hipMalloc(&s.descs, sizeof(xsknf_gpu_desc) * frames);
+      if (e == hipSuccess) e = hipMalloc(&s.verdicts, sizeof(int32_t) * frames);
+      if (e == hipSuccess) s.frames_cap = frames;
+    }
+    // the spare bytes past the span: defined (the loads that reach them are masked)
+    if (e == hipSuccess) e = hipMemsetAsync(s.umem + (s.b1 - s.b0), 0, 16, s.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) return hip_fail(e, "multi scatter: shard buffers");
+  }
+  // every shard at once: the root sends each its span and descriptors, every
+  // device receives its own (the root's to itself), one group
+  // (in pieces of kP2PPiece bytes)
+  static const uint64_t piece = getenv("XSKNF_MULTI_P2P_PIECE") ? strtoull(getenv("XSKNF_MULTI_P2P_PIECE"), nullptr, 0)
+                                                                 : kP2PPiece;   // DIAG (temporary)
+  const double t0 = now_s();
+  Shard &rs = m->sh[root];
+  ncclResult_t r = ncclGroupStart();
+  const auto pair = [&](const uint8_t *src, uint8_t *dst, uint64_t bytes, int k) {
+    for (uint64_t o = 0; o < bytes && r == ncclSuccess; o += piece) {
+      const size_t len = bytes - o < piece ? bytes - o : piece;
+      r = ncclSend(src + o, len, ncclUint8, k, m->comms[root], rs.stream);
+      if (r == ncclSuccess) r = ncclRecv(dst + o, len, ncclUint8, root, m->comms[k], m->sh[k].stream);
+    }
+  };
+  for (int k = 0; k < N && r == ncclSuccess; ++k) {
+    Shard &s = m->sh[k];
+    pair(umem + s.b0, s.umem, s.b1 - s.b0, k);
+    pair(reinterpret_cast<const uint8_t *>(m->root_descs + s.lo), reinterpret_cast<uint8_t *>(s.descs),
+         sizeof(xsknf_gpu_desc) * (s.hi - s.lo), k);
+  }
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess) return nccl_fail(r, "multi scatter: ncclSend / ncclRecv");
+  if (r2 != ncclSuccess) return nccl_fail(r2, "multi scatter: ncclGroupEnd");
+  for (Shard &s : m->sh) {
+    e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) return hip_fail(e, "multi scatter: wait");
+  }
+  if (seconds) *seconds = now_s() - t0;
+  m->root = root;
+  m->n = n;
+  return 0;
+}
+
+int xsknf_gpu_multi_process(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+                            uint32_t frame_len_max, uint32_t frame_len_mean, float *ms) {
+  if (!m || !opts || m->root < 0) return -EINVAL;
+  // every device's launches first (all in flight together), then the waits
+  for (Shard &s : m->sh) {
+    const uint64_t frames = s.hi - s.lo;
+    if (frames > UINT32_MAX) return -EINVAL;
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = hipEventRecord(s.e0, s.stream);
+    if (e != hipSuccess) return hip_fail(e, "multi process: start");
+    const int rc = xsknf_gpu_checksum_batch_lens(s.umem, s.b1 - s.b0, s.descs, static_cast<uint32_t>(frames),
+                                                 ingress_ifindex, opts, s.verdicts, frame_len_max, frame_len_mean,
+                                                 s.stream);
+    if (rc) return rc;
+    e = hipEventRecord(s.e1, s.stream);
+    if (e != hipSuccess) return hip_fail(e, "multi process: end");
+  }
+  for (int k = 0; k < m->ndev; ++k) {
+    Shard &s = m->sh[k];
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = hipEventSynchronize(s.e1);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, s.e0, s.e1);
+    if (e != hipSuccess) return hip_fail(e, "multi process: wait");
+    if (ms) ms[k] = t;
+  }
+  return 0;
+}
+
+int xsknf_gpu_multi_counters(struct xsknf_gpu_multi *m, uint64_t *out) {
+  if (!m || !out || m->root < 0) return -EINVAL;
+  for (Shard &s : m->sh) {
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess)
+      e = hipMemsetAsync(s.counters, 0, sizeof(unsigned long long) * XSKNF_GPU_MULTI_COUNTERS, s.stream);
+    const uint64_t frames = s.hi - s.lo;
+    if (e == hipSuccess && frames) {
+      const uint64_t want = (frames + 255) / 256;
+      const unsigned grid = static_cast<unsigned>(want < 2048 ? want : 2048);
+      hipLaunchKernelGGL(shard_counters, dim3(grid), dim3(256), 0, s.stream, s.umem, s.b1 - s.b0, s.descs,
+                         s.verdicts, frames, s.b0, s.counters);
+      e = hipGetLastError();
+    }
+    if (e != hipSuccess) return hip_fail(e, "multi counters: launch");
+  }
+  ncclResult_t r = ncclGroupStart();
+  for (int k = 0; k < m->ndev && r == ncclSuccess; ++k)
+    r = ncclAllReduce(m->sh[k].counters, m->sh[k].counters, XSKNF_GPU_MULTI_COUNTERS, ncclUint64, ncclSum,
+                      m->comms[k], m->sh[k].stream);
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess) return nccl_fail(r, "multi counters: ncclAllReduce");
+  if (r2 != ncclSuccess) return nccl_fail(r2, "multi counters: ncclGroupEnd");
+  for (Shard &s : m->sh) {
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) return hip_fail(e, "multi counters: wait");
+  }
+  // every device holds the sum; the root's copy is the answer
+  Shard &rs = m->sh[m->root];
+  hipError_t e = hipSetDevice(rs.device);
+  if (e == hipSuccess)
+    e = hipMemcpy(out, rs.counters, sizeof(unsigned long long) * XSKNF_GPU_MULTI_COUNTERS, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? 0 : hip_fail(e, "multi counters: copy");
+}
+
+int xsknf_gpu_multi_shard_info(const struct xsknf_gpu_multi *m, int k, struct xsknf_gpu_shard_info *info) {
+  if (!m || !info || k < 0 || k >= m->ndev) return -EINVAL;
+  const Shard &s = m->sh[k];
+  info->device = s.device;
+  info->reserved = 0;
+  info->frame_lo = s.lo;
+  info->frame_hi = s.hi;
+  info->span_lo = s.b0;
+  info->span_hi = s.b1;
+  info->frame_bytes = s.bytes;
+  info->umem = s.umem;
+  info->descs = s.descs;
+  info->verdicts = s.verdicts;
+  return 0;
+}
+
+int xsknf_gpu_multi_fetch(const struct xsknf_gpu_multi *m, int k, uint8_t *umem_out, struct xsknf_gpu_desc *descs_out,
+                          int32_t *verdicts_out) {
+  if (!m || k < 0 || k >= m->ndev || m->root < 0) return -EINVAL;
+  const Shard &s = m->sh[k];
+  hipError_t e = hipSetDevice(s.device);
+  if (e == hipSuccess && umem_out && s.b1 > s.b0)
+    e = hipMemcpy(umem_out, s.umem, s.b1 - s.b0, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && descs_out && s.hi > s.lo)
+    e = hipMemcpy(descs_out, s.descs, sizeof(xsknf_gpu_desc) * (s.hi - s.lo), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && verdicts_out && s.hi > s.lo)
+    e = hipMemcpy(verdicts_out, s.verdicts, sizeof(int32_t) * (s.hi - s.lo), hipMemcpyDeviceToHost);
+  return e == hipSuccess ? 0 : hip_fail(e, "multi fetch");
+}
+
+int xsknf_gpu_multi_destroy(struct xsknf_gpu_multi *m) {
+  if (!m) return -EINVAL;
+  for (Shard &s : m->sh) {
+    if (hipSetDevice(s.device) != hipSuccess) continue;
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.umem) (void)hipFree(s.umem);
+    if (s.descs) (void)hipFree(s.descs);
+    if (s.verdicts) (void)hipFree(s.verdicts);
+    if (s.counters) (void)hipFree(s.counters);
+    if (s.e0) (void)hipEventDestroy(s.e0);
+    if (s.e1) (void)hipEventDestroy(s.e1);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  if (m->root_descs && hipSetDevice(m->root_descs_dev) == hipSuccess) (void)hipFree(m->root_descs);
+  for (ncclComm_t c : m->comms)
+    if (c) (void)ncclCommDestroy(c);
+  delete m;
+  return 0;
+}
+
+}  // extern "C"

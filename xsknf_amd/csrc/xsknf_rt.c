@@ -787,7 +787,12 @@ static void *worker_loop(void *arg)
 	return NULL;
 }
 
-/* ---- argument parsing (src/xsknf.c:744-870) ---- */
+/* ---- argument parsing ----
+ * The library's command line is the reference's contract (src/xsknf.c:744-874):
+ * the same short options ("i:pSf:ub:BM:w:"), long names and meanings, parsed up
+ * to the `--` that starts the application's own options, and a process that
+ * gets a bad option ends with status 1 after printing what was wrong and the
+ * option summary.  The wording of the messages is this runtime's own. */
 
 static const struct option long_options[] = {
 	{"iface", required_argument, 0, 'i'},
@@ -802,107 +807,99 @@ static const struct option long_options[] = {
 	{0, 0, 0, 0},
 };
 
-static void usage(void)
+static const struct {
+	const char *flags, *text;
+} option_help[] = {
+	{"-i, --iface=IF[:c|z]", "receive on interface IF (repeatable); :c forces copy mode, :z zero-copy"},
+	{"-p, --poll", "wait for traffic with poll() instead of spinning"},
+	{"-S, --xdp-skb", "attach the redirect program in generic (skb) mode"},
+	{"-f, --frame-size=N", "UMEM chunk size in bytes (a power of two unless -u)"},
+	{"-u, --unaligned", "unaligned chunk mode: frames at any UMEM offset"},
+	{"-b, --batch-size=N", "rx/tx descriptors handled per ring pass"},
+	{"-B, --busy-poll", "request busy polling on the sockets"},
+	{"-M, --mode=MODE", "AF_XDP (the only mode this runtime runs), XDP or COMBINED"},
+	{"-w, --workers=N", "worker threads, one rx queue each"},
+};
+
+static void __attribute__((noreturn)) bad_args(const char *fmt, const char *arg)
 {
-	fprintf(stderr,
-		"	xsknf options:\n"
-		"	-i, --iface=n[:m]	Interface to operate on (a copy mode between copy (c) or zero-copy (z)\n"
-		"				can optionally be specified). Can be repeated multiple times\n"
-		"	-p, --poll		Use poll syscall\n"
-		"	-S, --xdp-skb=n		Use XDP skb-mode\n"
-		"	-f, --frame-size=n	Set the frame size (must be a power of two in aligned mode, default is %d)\n"
-		"	-u, --unaligned		Enable unaligned chunk placement\n"
-		"	-b, --batch-size=n	Batch size for sending or receiving packets. Default is %u\n"
-		"	-B, --busy-poll		Busy poll\n"
-		"	-M  --mode		Working mode (AF_XDP, XDP, COMBINED)\n"
-		"	-w  --workers=n		Number of packet processing workers\n"
-		"\n",
+	if (fmt)
+		fprintf(stderr, fmt, arg);
+	fprintf(stderr, "xsknf library options (before `--`; frame size default %d, batch size default %u):\n",
 		DEFAULT_FRAME_SIZE, default_conf.batch_size);
+	for (size_t k = 0; k < sizeof(option_help) / sizeof(option_help[0]); k++)
+		fprintf(stderr, "  %-24s %s\n", option_help[k].flags, option_help[k].text);
 	exit(EXIT_FAILURE);
+}
+
+// "IF" or "IF:c" / "IF:z": the interface name (the suffix cut off in place) and its bind flags
+static void add_interface(struct xsknf_config *config, char *spec)
+{
+	if (config->num_interfaces >= XSKNF_MAX_INTERFACES)
+		bad_args("xsknf: more interfaces than XSKNF_MAX_INTERFACES (at '%s')\n", spec);
+	uint32_t flags = DEFAULT_BIND_FLAGS;
+	char *mode = strchr(spec, ':');
+	if (mode) {
+		if (!strcmp(mode + 1, "c"))
+			flags |= XDP_COPY;
+		else if (!strcmp(mode + 1, "z"))
+			flags |= XDP_ZEROCOPY;
+		else
+			bad_args("xsknf: copy mode '%s' is neither c nor z\n", mode + 1);
+		*mode = 0;
+	}
+	config->bind_flags[config->num_interfaces] = flags;
+	config->interfaces[config->num_interfaces++] = spec;
+}
+
+static int working_mode_of(const char *name)
+{
+	static const struct {
+		const char *name;
+		int mode;
+	} modes[] = {{"AF_XDP", MODE_AF_XDP}, {"XDP", MODE_XDP}, {"COMBINED", MODE_COMBINED}};
+	for (size_t k = 0; k < sizeof(modes) / sizeof(modes[0]); k++)
+		if (!strcmp(name, modes[k].name))
+			return modes[k].mode;
+	bad_args("xsknf: no working mode named '%s'\n", name);
 }
 
 int xsknf_parse_args(int argc, char **argv, struct xsknf_config *config)
 {
-	int option_index, c;
 	memcpy(config, &default_conf, sizeof(*config));
 	snprintf(config->ebpf_filename, sizeof(config->ebpf_filename), "%s_kern.o", argv[0]);
 	snprintf(config->xdp_progname, sizeof(config->xdp_progname), "handle_xdp");
 	config->tc_progname[0] = 0;
 
+	int c, option_index;
 	while ((c = getopt_long(argc, argv, "i:pSf:ub:BM:w:", long_options, &option_index)) != -1) {
 		switch (c) {
-		case 'i': {
-			if (config->num_interfaces >= XSKNF_MAX_INTERFACES) {
-				fprintf(stderr, "ERROR: too many interfaces\n");
-				usage();
-			}
-			uint32_t flags = DEFAULT_BIND_FLAGS;
-			char *colon = strchr(optarg, ':');
-			if (colon) {
-				if (colon[1] == 'c') {
-					flags |= XDP_COPY;
-				} else if (colon[1] == 'z') {
-					flags |= XDP_ZEROCOPY;
-				} else {
-					fprintf(stderr, "ERROR: unknown copy mode '%c'\n", colon[1]);
-					usage();
-				}
-				*colon = 0;
-			}
-			config->bind_flags[config->num_interfaces] = flags;
-			config->interfaces[config->num_interfaces++] = optarg;
-			break;
-		}
-		case 'p':
-			config->poll = 1;
-			break;
-		case 'S':
-			config->xdp_flags |= XDP_FLAGS_SKB_MODE;
-			break;
-		case 'u':
-			config->unaligned_chunks = 1;
-			break;
-		case 'f':
-			config->xsk_frame_size = atoi(optarg);
-			break;
-		case 'b':
-			config->batch_size = (uint32_t)atoi(optarg);
-			break;
-		case 'B':
-			config->busy_poll = 1;
-			break;
-		case 'M':
-			if (!strcmp(optarg, "AF_XDP")) {
-				config->working_mode = MODE_AF_XDP;
-			} else if (!strcmp(optarg, "XDP")) {
-				config->working_mode = MODE_XDP;
-			} else if (!strcmp(optarg, "COMBINED")) {
-				config->working_mode = MODE_COMBINED;
-			} else {
-				fprintf(stderr, "ERROR: unknown working mode %s\n", optarg);
-				usage();
-			}
-			break;
+		case 'i': add_interface(config, optarg); break;
+		case 'p': config->poll = 1; break;
+		case 'S': config->xdp_flags |= XDP_FLAGS_SKB_MODE; break;
+		case 'u': config->unaligned_chunks = 1; break;
+		case 'f': config->xsk_frame_size = atoi(optarg); break;
+		case 'b': config->batch_size = (uint32_t)atoi(optarg); break;
+		case 'B': config->busy_poll = 1; break;
+		case 'M': config->working_mode = working_mode_of(optarg); break;
 		case 'w':
 			config->workers = (unsigned)atoi(optarg);
-			if (config->workers < 1) {
-				fprintf(stderr, "ERROR: Invalid number of workers %u", config->workers);
-				usage();
-			}
+			if (config->workers < 1)
+				bad_args("xsknf: worker count '%s' is not a positive number\n", optarg);
 			break;
-		default:
-			usage();
+		default:   // getopt has already said what it did not understand
+			bad_args(NULL, NULL);
 		}
 	}
-	if (config->num_interfaces == 0) {
-		fprintf(stderr, "ERROR: at least one interface in required\n");
-		usage();
-	}
+	if (config->num_interfaces == 0)
+		bad_args("%sxsknf: no interface given (-i IF)\n", "");
 	if (!(config->xdp_flags & XDP_FLAGS_SKB_MODE))
 		config->xdp_flags |= XDP_FLAGS_DRV_MODE;
-	if ((config->xsk_frame_size & (config->xsk_frame_size - 1)) && !config->unaligned_chunks) {
-		fprintf(stderr, "--frame-size=%d is not a power of two\n", config->xsk_frame_size);
-		usage();
+	const unsigned fs = (unsigned)config->xsk_frame_size;
+	if (!config->unaligned_chunks && (fs & (fs - 1))) {
+		char num[16];
+		snprintf(num, sizeof(num), "%d", config->xsk_frame_size);
+		bad_args("xsknf: frame size %s must be a power of two without -u\n", num);
 	}
 	return 0;
 }
