@@ -34,6 +34,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 # pageable host copies through HIP's own staging buffers, not by locking the
@@ -108,6 +109,8 @@ def parse():
     p.add_argument("--no-probes", action="store_true", help="skip the read / step-floor probes")
     p.add_argument("--no-c-host-multi", action="store_true",
                    help="world 1: skip config 4 through the C host's multi-device calls (`c_host_multi`)")
+    p.add_argument("--c-host-multi-timeout", type=float, default=240.0,
+                   help="seconds before the `c_host_multi` leg is abandoned (the line is printed without it)")
     p.add_argument("--no-verify", action="store_true",
                    help="skip the RFC receive-side check of the primary and config4 outputs (rfc_check)")
     p.add_argument("--rotate", type=int, default=0,
@@ -587,6 +590,28 @@ def c_host_multi_leg(args, dev, reps=10):
                    f"{reps} steps, each the slowest device's HIP-event time"}
 
 
+def bounded_leg(fn, seconds, line):
+    """Run one optional leg with a watchdog: its result, {"error": ...} if it
+    raised, and if it has not returned after `seconds` the bench line is printed
+    with {"error": "timed out"} in its place and the process exits 0 (the
+    primary's figures stand; the exit ends whatever the leg left on the GPU)."""
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(seconds):
+            line["c_host_multi"] = {"error": f"timed out after {seconds} s (the line was printed by the watchdog)"}
+            print(json.dumps(line), flush=True)
+            os._exit(0)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        return fn()
+    except Exception as e:   # reported in the line; the primary's figures stand
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        done.set()
+
+
 def check_fingerprint(umem, descs, base):
     """[sum of the written checks, the same weighted by (global offset mod 65521) + 1]
     over the well-formed-length frames of one batch (device tensors; `base` =
@@ -842,12 +867,6 @@ def main():
             torch.cuda.empty_cache()
 
     root_scatter = root_scatter_leg(args, world, rank, dev) if (_DIST and not args.no_root_scatter) else None
-    c_multi = None
-    if world == 1 and not args.no_c_host_multi:
-        try:
-            c_multi = c_host_multi_leg(args, dev)
-        except Exception as e:   # reported in the line; the primary's figures stand
-            c_multi = {"error": f"{type(e).__name__}: {e}"}
     # what the collectives saw: every rank contributes 1 (so a SCALE line shows
     # that the backend really had N ranks), and the frames summed over ranks
     dist_info = None
@@ -933,10 +952,12 @@ def main():
             out["config"]["rehearsal"] = rehearsal
         if root_scatter is not None:
             out["root_scatter"] = root_scatter
-        if c_multi is not None:
-            out["c_host_multi"] = c_multi
         if dist_info is not None:
             out["dist"] = dist_info
+        if world == 1 and not args.no_c_host_multi:
+            # last, and bounded: on a node of several GPUs this is one process
+            # driving all of them over RCCL; a hang there must not cost the line
+            out["c_host_multi"] = bounded_leg(lambda: c_host_multi_leg(args, dev), args.c_host_multi_timeout, out)
         print(json.dumps(out), flush=True)
     if _DIST:
         dist.destroy_process_group()

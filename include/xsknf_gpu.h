@@ -388,6 +388,14 @@ XSKNF_GPU_API int xsknf_gpu_multi_destroy(struct xsknf_gpu_multi *m);
  * private to the calling thread). */
 XSKNF_GPU_API const char *xsknf_gpu_last_error(void);
 
+/* Pool guard of the current device (synchronizes it first): how many waves of
+ * the pooled split kernel found a unit of their block that no wave claimed
+ * (its frames left unsummed).  The launch's grid bound makes this unreachable;
+ * a nonzero count is a library bug.  reset != 0 zeroes the count after reading.
+ * No reference counterpart (a device-side invariant check for tests and
+ * monitoring). */
+XSKNF_GPU_API int xsknf_gpu_pool_guard_trips(uint32_t *trips, int reset);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -46,7 +46,9 @@ def main():
     torch.cuda.synchronize()
     gv, gu = v.cpu().numpy(), umem.cpu().numpy()
     _, ov = oracles.time_batch(host, hd)
+    from xsknf_amd import _lib
     print(json.dumps({"frames": n, "cus_limit": os.environ.get("XSKNF_GPU_CU_LIMIT"),
+                      "pool_guard_trips": _lib.pool_guard_trips(),
                       "window_chunks": int(cs.launch_cfg().window_chunks),
                       "bad_verdicts": int((gv != ov).sum()), "bad_bytes": int((gu != host).sum())}))
 

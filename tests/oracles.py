@@ -8,6 +8,8 @@ batch-64 loop (src/xsknf.c:654-672) split over threads.  It is required: a GPU
 run without it fails (there is no quiet fall back to the restatement, which
 tests/test_ref_pin.py holds equal to it on CPU).
 """
+import numpy as np
+
 from oracle import ref as R
 
 KIND = "reference"
@@ -22,6 +24,23 @@ def require():
 
 
 def time_batch(umem, descs, threads=16, **kw):
-    """In place over the host batch; returns (seconds, verdicts)."""
+    """In place over the host batch; returns (seconds, verdicts).
+
+    The reference never sees a descriptor outside its UMEM: the kernel's rx
+    validation drops it before the ring (and xsknf_gpu's boundary gives it -1,
+    untouched, include/xsknf_gpu.h).  Such descriptors get -1 here and only the
+    others go to the reference's function, whose pointer arithmetic
+    (src/xsknf.c:659) would otherwise leave the buffer."""
     require()
-    return R.time_batch(umem, descs, threads=threads, reps=1, pin=False, **kw)
+    a = descs["addr"].astype(np.uint64)
+    off = (a & np.uint64((1 << 48) - 1)) + (a >> np.uint64(48))
+    size = np.uint64(umem.size)
+    ok = (off <= size) & (descs["len"].astype(np.uint64) <= size - np.minimum(off, size))
+    if ok.all():
+        return R.time_batch(umem, descs, threads=threads, reps=1, pin=False, **kw)
+    v = np.full(descs.shape[0], -1, dtype=np.int32)
+    if ok.any():
+        t, v[ok] = R.time_batch(umem, np.ascontiguousarray(descs[ok]), threads=threads, reps=1, pin=False, **kw)
+    else:
+        t = 0.0
+    return t, v

@@ -20,6 +20,17 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _pool_guard_never_trips():
+    """Every launch of this module, and of the modules before it: no wave of the
+    pooled split kernel found a unit of its block unclaimed (the device counter
+    behind xsknf_gpu_pool_guard_trips; ADVICE r05: the grid bound is the only
+    thing that keeps a pooled block's units inside its patch lists)."""
+    yield
+    from xsknf_amd import _lib
+    assert _lib.pool_guard_trips() == 0
+
+
 def _results(*tensors):
     """The launch's outputs on the host BEFORE any CPU oracle work: a fault in
     the launch is then reported here, inside the test that made it (HIP reports
@@ -1043,6 +1054,7 @@ def test_grid_sizing_on_a_smaller_device(length, n, window):
     assert r["cus_limit"] == "4"
     assert r["window_chunks"] == window   # the shape the product picks: jumbo / W = 8 pooled, static, lane
     assert r["bad_verdicts"] == 0 and r["bad_bytes"] == 0, r
+    assert r["pool_guard_trips"] == 0, r
 
 
 @pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 18, 1, 52), (16, 3, 2, 0, 0, 1, 52),

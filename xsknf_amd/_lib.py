@@ -19,6 +19,7 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_device_count",
     "xsknf_gpu_checksum_batch",
     "xsknf_gpu_last_error",
+    "xsknf_gpu_pool_guard_trips",
     "xsknf_gpu_default_launch_cfg",
     "xsknf_gpu_checksum_batch_cfg",
     "xsknf_gpu_checksum_batch_lens",
@@ -222,8 +223,19 @@ def load() -> ctypes.CDLL:
     lib.xsknf_gpu_multi_fetch.argtypes = [vp, ctypes.c_int, vp, vp, vp]
     lib.xsknf_gpu_multi_destroy.restype = ctypes.c_int
     lib.xsknf_gpu_multi_destroy.argtypes = [vp]
+    lib.xsknf_gpu_pool_guard_trips.restype = ctypes.c_int
+    lib.xsknf_gpu_pool_guard_trips.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     _lib = lib
     return lib
+
+
+def pool_guard_trips(reset: bool = False) -> int:
+    """Waves of the pooled split kernel on the current device that found a unit
+    no wave claimed (include/xsknf_gpu.h xsknf_gpu_pool_guard_trips; 0 unless
+    the library's grid bound is wrong)."""
+    t = ctypes.c_uint32(0)
+    check(load().xsknf_gpu_pool_guard_trips(ctypes.byref(t), 1 if reset else 0), "xsknf_gpu_pool_guard_trips")
+    return int(t.value)
 
 
 def last_error() -> str:

@@ -1181,6 +1181,20 @@ constexpr uint32_t pool_parts(int w) { return w == 4 ? 4u : 2u; }
 // halved instead of 12 at 1500 B: 276.5-277.5 and 277.5-278.5 vs 277.3-278.3
 // us, NIC +0.5..1 -- profiles/r05/ab/ab_halves_tiles_*).
 constexpr uint32_t pool_split_tiles(int w, int sw) { return w == 4 ? 3u * sw : static_cast<uint32_t>(sw); }
+// The most tiles one pool block may hold so that its units fit its waves'
+// patch lists (SW x PT entries): bt tiles, the last pool_split_tiles of them in
+// pool_parts units each, are bt + (parts - 1) x split units.  launch_split sizes
+// the grid by it and the kernel asserts the same count, so the two cannot drift.
+constexpr uint32_t pool_block_tiles_max(int w, int sw, int pt) {
+  return static_cast<uint32_t>(sw * pt) - (pool_parts(w) - 1) * pool_split_tiles(w, sw);
+}
+
+// Pool guard: a pooled wave whose patch list is full claims no more units, so
+// a grid too small for the batch would leave units unclaimed (their frames
+// unsummed).  launch_split's bound makes that unreachable; should it ever be
+// reached, the block's patch queue waits for a unit that never comes, and each
+// wave that gives up counts here (xsknf_gpu_pool_guard_trips reads it).
+__device__ unsigned int g_pool_guard_trips;
 
 // The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
 // a 20-unit list (80 KiB of its block's 151 KiB; 16 units until the late
@@ -1395,6 +1409,8 @@ void checksum_kernel_split(const KernelArgs args) {
   constexpr bool kShared = PT > 0 && kPool;
   constexpr uint32_t kPQ = kShared ? SW * PT : 1;   // marks: the grid is sized so a block has <= SW * PT units
   constexpr uint32_t kPQNull = 0xffffu;
+  static_assert(!kShared || pool_block_tiles_max(W, SW, PT) + (pool_parts(W) - 1) * pool_split_tiles(W, SW) == kPQ,
+                "a pool block at launch_split's tile bound has exactly as many units as its lists hold");
   __shared__ uint32_t pq_tail, pq_head;
   __shared__ uint32_t pq[kPQ];
   const bool shared_on = kShared && list_ok;   // block-uniform
@@ -1656,7 +1672,10 @@ void checksum_kernel_split(const KernelArgs args) {
             if (m != 0 || wall_clock64() - tw0 > 2000000ull) break;   // 20 ms: never, unless units went unclaimed
             __builtin_amdgcn_s_sleep(2);
           }
-          if (m == 0) break;
+          if (m == 0) {   // a unit no wave claimed: its frames are unsummed (never, by the grid bound)
+            if (lane == 0) __hip_atomic_fetch_add(&g_pool_guard_trips, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
           if (m != kPQNull) {
             const uint32_t w2 = (m - 1) >> 8, t2 = (m - 1) & 0xffu;
             tail_patch_list(args, lds_addr(&plist[w2][0]) + 8 * t2 * kWave, 1, lane);
@@ -2249,7 +2268,7 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
       // SW * (PT - (parts - 1) * k) tiles -- the jumbo shape's 20-unit lists with
       // the last 3 SW tiles in quarters hold 88 tiles (64 at 1M frames on 256
       // CUs); until round 5 the bound was SW * (PT - 1), 120)
-      constexpr uint32_t per_block = pooled_split(SW) ? SW * PT - (pool_parts(W) - 1) * pool_split_tiles(W, SW) : SW * PT;
+      constexpr uint32_t per_block = pooled_split(SW) ? pool_block_tiles_max(W, SW, PT) : SW * PT;
       const uint32_t fit = (tiles + per_block - 1) / per_block;
       if (grid < fit) grid = fit;
     }
@@ -2532,6 +2551,21 @@ int xsknf_gpu_launch_cfg_for_lens(uint32_t frame_len_max, uint32_t frame_len_mea
                                   struct xsknf_gpu_launch_cfg *cfg) {
   if (!cfg) return -EINVAL;
   xsknf_gpu::default_cfg(frame_len_max ? frame_len_max : 2048u, *cfg, frame_len_mean);
+  return 0;
+}
+
+int xsknf_gpu_pool_guard_trips(uint32_t *trips, int reset) {
+  if (!trips) return -EINVAL;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(trips, HIP_SYMBOL(xsknf_gpu::g_pool_guard_trips), sizeof(*trips));
+  if (e == hipSuccess && reset) {
+    const uint32_t zero = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(xsknf_gpu::g_pool_guard_trips), &zero, sizeof(zero));
+  }
+  if (e != hipSuccess) {
+    xsknf_gpu::set_error(e, "xsknf_gpu_pool_guard_trips");
+    return -EIO;
+  }
   return 0;
 }
 

@@ -41,7 +41,14 @@ namespace {
 
 constexpr uint64_t kOutOfRange = 1ull << 47;   // an address past any UMEM: verdict -1, no bytes
 constexpr uint32_t kFingerprintMod = 65521;
-constexpr uint64_t kP2PPiece = 1ull << 28;     // bytes per ncclSend / ncclRecv of a scatter
+// Bytes per ncclSend / ncclRecv of a scatter.  One ncclSend of a whole span
+// past 1 GiB delivered only part of it with this image's RCCL (a send to self
+// of the 2 GiB and 16 GiB spans of 1M and 8M IMIX frames: the bytes from 1 GiB
+// on -- from 2 GiB on in 4 GiB pieces -- never arrived, while the calls and the
+// group returned success); 256 MiB pieces delivered every byte
+// (profiles/r06/multi_p2p_pieces.jsonl; the probe, with the piece size as an
+// environment knob, is in commit cca61bb's tools/diag_multi_p2p.py).
+constexpr uint64_t kP2PPiece = 1ull << 28;
 
 __host__ __device__ inline uint64_t umem_offset(uint64_t addr) {
   return (addr & XSKNF_GPU_UNALIGNED_BUF_ADDR_MASK) + (addr >> XSKNF_GPU_UNALIGNED_BUF_OFFSET_SHIFT);
@@ -298,10 +305,9 @@ int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, const uint8_t *
     if (e != hipSuccess) return hip_fail(e, "multi scatter: shard buffers");
   }
   // every shard at once: the root sends each its span and descriptors, every
-  // device receives its own (the root's to itself), one group
-  // (in pieces of kP2PPiece bytes)
-  static const uint64_t piece = getenv("XSKNF_MULTI_P2P_PIECE") ? strtoull(getenv("XSKNF_MULTI_P2P_PIECE"), nullptr, 0)
-                                                                 : kP2PPiece;   // DIAG (temporary)
+  // device receives its own (the root's to itself), one group, in pieces of
+  // kP2PPiece bytes
+  const uint64_t piece = kP2PPiece;
   const double t0 = now_s();
   Shard &rs = m->sh[root];
   ncclResult_t r = ncclGroupStart();
