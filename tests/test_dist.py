@@ -63,11 +63,14 @@ def test_two_rank_gloo_shards_and_counters():
     assert total[2] + total[3] == b.n
 
 
-def _root_worker(rank, world, port, out):
+def _root_worker(rank, world, port, out, piece=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import csum_oracle as O
+    from xsknf_amd import shard
     from xsknf_amd.shard import scatter_from_root
+    if piece:
+        shard.P2P_PIECE = piece      # several messages per span, as past 256 MiB on the GPU
     umem = descs = ranges = None
     if rank == 0:
         b = frames.unaligned_batch(3000, "imix", seed=21)
@@ -83,15 +86,16 @@ def _root_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_root_scatter_shards_are_bit_exact(world):
+@pytest.mark.parametrize("world,piece", [(2, None), (3, None), (3, 4099)])
+def test_root_scatter_shards_are_bit_exact(world, piece):
     """bench.py --root-scatter's distribution (collective 1) on
     gloo: every rank checksums the shard it received, and the bytes and
-    verdicts equal the oracle's pass over the whole batch on the root."""
+    verdicts equal the oracle's pass over the whole batch on the root; also
+    with every span sent as many pieces (shard.P2P_PIECE, 256 MiB on the GPU)."""
     from oracle import csum_oracle as O
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_root_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_root_worker, args=(world, _free_port(), out, piece), nprocs=world, join=True)
     b = frames.unaligned_batch(3000, "imix", seed=21)
     frames.inject_edge_cases(b, 0.05, seed=22)
     ranges = shard_by_bytes(b.descs["len"], world)

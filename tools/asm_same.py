@@ -11,6 +11,12 @@ REV still describe the product's kernels:
 
 --diff prints the instruction diff of every kernel that is not identical
 (a renamed twin is matched by name with its template arguments removed).
+
+    python3 tools/asm_same.py --ab
+
+compares every product kernel with the kernel of the same name in the A/B build
+(`make ab` -> build/ab/checksummer-gfx950.s): the A/B switches live in
+checksummer_ab.h, and the shared kernels must be instruction-identical.
 """
 import difflib
 import os
@@ -45,7 +51,28 @@ def kernels(path):
     return out
 
 
+def vs_ab():
+    subprocess.run(["make", "-C", ROOT, "asm", "ab"], check=True, stdout=subprocess.DEVNULL)
+    only_k = lambda d: {k: v for k, v in d.items() if "kernel" in k}   # (device globals match the pattern too)
+    a = only_k(kernels(os.path.join(ROOT, "build", "asm", "checksummer-gfx950.s")))
+    b = only_k(kernels(os.path.join(ROOT, "build", "ab", "checksummer-gfx950.s")))
+    # the same instructions, scheduled or register-assigned differently
+    regs = lambda ins: sorted(re.sub(r"\b([vs])(\d+)\b|\b([vs])\[\d+:\d+\]", r"\1\3#", x) for x in ins)
+    same = [k for k in sorted(a) if k in b and a[k] == b[k]]
+    renamed = [k for k in sorted(a) if k in b and a[k] != b[k] and regs(a[k]) == regs(b[k])]
+    bad = [k for k in sorted(a) if k not in b or regs(a[k]) != regs(b[k])]
+    for k in renamed:
+        print(f"same instructions, scheduled / register-assigned differently: {k}")
+    for k in bad:
+        print(f"differs: {k}" if k in b else f"not in the A/B build: {k}")
+    print(f"{len(same)} product kernels identical in the A/B build, {len(renamed)} the same instructions "
+          f"scheduled or register-assigned differently, {len(bad)} not ({len(set(b) - set(a))} A/B-only kernels)")
+    return 0 if not bad else 1
+
+
 def main():
+    if sys.argv[1:] == ["--ab"]:
+        return vs_ab()
     args = [a for a in sys.argv[1:] if a != "--diff"]
     show = "--diff" in sys.argv[1:]
     if len(args) != 1:

@@ -96,6 +96,13 @@ def rebase_descs(descs, b0: int, umem_size: int) -> np.ndarray:
     return out
 
 
+# Bytes per point-to-point message of the root distribution: one RCCL send of
+# more than 1 GiB delivered only part of its bytes on this image (the C host's
+# scatter, xsknf_amd/csrc/multi.hip kP2PPiece; profiles/r06/multi_p2p_pieces.jsonl),
+# so spans go in 256 MiB pieces (matched send for send on both sides).
+P2P_PIECE = 1 << 28
+
+
 def scatter_from_root(dist, umem, descs, ranges, rank: int, world: int, device, root: int = 0):
     """Move every rank's shard from the root.  On the root: `umem` is the whole
     UMEM (uint8 tensor on `device`), `descs` the whole descriptor array
@@ -121,13 +128,15 @@ def scatter_from_root(dist, umem, descs, ranges, rank: int, world: int, device, 
             if r == root:
                 local = (umem[rb0:rb1], d)
             else:
-                ops.append(dist.P2POp(dist.isend, umem[rb0:rb1].contiguous(), r))
+                for o in range(rb0, rb1, P2P_PIECE):
+                    ops.append(dist.P2POp(dist.isend, umem[o:min(o + P2P_PIECE, rb1)].contiguous(), r))
                 ops.append(dist.P2POp(dist.isend, d, r))
     else:
         # 16 spare bytes: the kernel's 16-byte chunk loads may end past the span
         buf = torch.empty(b1 - b0 + 16, dtype=torch.uint8, device=device)
         d = torch.empty((n, 2), dtype=torch.int64, device=device)
-        ops.append(dist.P2POp(dist.irecv, buf[:b1 - b0], root))
+        for o in range(0, b1 - b0, P2P_PIECE):
+            ops.append(dist.P2POp(dist.irecv, buf[o:min(o + P2P_PIECE, b1 - b0)], root))
         ops.append(dist.P2POp(dist.irecv, d, root))
         local = (buf, d)
     if ops:
