@@ -596,11 +596,19 @@ def bounded_leg(fn, seconds, line):
     with {"error": "timed out"} in its place and the process exits 0 (the
     primary's figures stand; the exit ends whatever the leg left on the GPU)."""
     done = threading.Event()
+    # what the leg's libraries print to stdout (RCCL's version banner at
+    # communicator init) goes to stderr: stdout carries the one JSON line
+    sys.stdout.flush()
+    saved, py_stdout = os.dup(1), sys.stdout
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
 
     def watchdog():
         if not done.wait(seconds):
+            os.dup2(saved, 1)
             line["c_host_multi"] = {"error": f"timed out after {seconds} s (the line was printed by the watchdog)"}
-            print(json.dumps(line), flush=True)
+            py_stdout.write(json.dumps(line) + "\n")
+            py_stdout.flush()
             os._exit(0)
 
     threading.Thread(target=watchdog, daemon=True).start()
@@ -610,6 +618,9 @@ def bounded_leg(fn, seconds, line):
         return {"error": f"{type(e).__name__}: {e}"}
     finally:
         done.set()
+        sys.stdout = py_stdout
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def check_fingerprint(umem, descs, base):

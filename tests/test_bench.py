@@ -2,6 +2,8 @@
 keeps a pass out of the Infinity Cache, the iteration schedule that makes every
 step rewrite every check of a base workload, the stream / batch pairing of
 --streams, and the NIC workloads' shapes."""
+import os
+
 import numpy as np
 import pytest
 
@@ -116,3 +118,42 @@ def test_lane_batch_workload_is_thirteen_batches():
         config4_frames = 8192
     lens, span = bench.workload_lengths("64-13M", A, 1, 0)
     assert lens.shape[0] == 13 * 1024 and span is None and int(lens.max()) == 64
+
+
+_LEG_CHILD = r"""
+import os, sys, time
+sys.path.insert(0, {root!r})
+import bench
+line = {{"metric": "m", "value": 1}}
+def leg():
+    os.write(1, b"RCCL version : banner\n")   # a library writing to fd 1, as RCCL's init does
+    print("from python")
+    if {sleep}:
+        time.sleep({sleep})
+    return {{"ok": True}}
+line["c_host_multi"] = bench.bounded_leg(leg, {timeout}, line)
+print(__import__("json").dumps(line), flush=True)
+"""
+
+
+@pytest.mark.parametrize("sleep,timeout", [(0, 30), (30, 1)])
+def test_bounded_leg_keeps_stdout_to_one_line(sleep, timeout):
+    """The `c_host_multi` leg (one process over every device of the node) runs
+    last, its libraries' stdout (RCCL's version banner) goes to stderr, and if
+    it hangs past the timeout the watchdog prints the line without it and the
+    process exits 0: stdout always holds exactly one JSON line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _LEG_CHILD.format(root=root, sleep=sleep, timeout=timeout)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = p.stdout.strip().splitlines()
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert "RCCL version" in p.stderr and "from python" in p.stderr
+    if sleep:
+        assert "timed out" in out["c_host_multi"]["error"]
+    else:
+        assert out["c_host_multi"] == {"ok": True}
