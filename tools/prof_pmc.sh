@@ -11,5 +11,5 @@ export TMPDIR=/tmp
 cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d "$OUT/$C" -o run \
-      -- python3 "$R/bench.py" --cpu-seconds 0 --no-probes --secondary "" "$@" > "$OUT/$C.bench.json" 2> "$OUT/$C.stderr.log"
+      -- python3 "$R/bench.py" --cpu-seconds 0 --no-probes --no-c-host-multi --secondary "" "$@" > "$OUT/$C.bench.json" 2> "$OUT/$C.stderr.log"
 done

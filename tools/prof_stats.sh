@@ -9,4 +9,4 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run \
-    -- python3 "$R/bench.py" --cpu-seconds 0 --no-probes --secondary "" "$@" > "$OUT/bench.json" 2> "$OUT/stderr.log"
+    -- python3 "$R/bench.py" --cpu-seconds 0 --no-probes --no-c-host-multi --secondary "" "$@" > "$OUT/bench.json" 2> "$OUT/stderr.log"

@@ -33,9 +33,9 @@ def main():
     main_name = rows[0][1]
     # a batch of more than 1M frames runs as 1M-frame launches (config 4 on one GPU)
     # (the lane kernel, frames <= 128 B, takes up to 16M frames per launch)
-    per_step = -(-int(bench["config"]["frames_per_gpu"]) // (1 << (24 if int(bench["config"].get("frame_len") or 0) == 64 and
-                                                                       "lane" in bench["roofline"].get("kernels", "")
-                                                                       else 20)))
+    # (frame_len is a string for a mix: "imix")
+    lane64 = str(bench["config"].get("frame_len")) == "64" and "lane" in bench["roofline"].get("kernels", "")
+    per_step = -(-int(bench["config"]["frames_per_gpu"]) // (1 << (24 if lane64 else 20)))
     ksteps = int(bench.get("kernel_steps", 50))
     tail = per_step * (3 + ksteps) if kalone else 0
     mains = [r for r in rows if r[1] == main_name]

@@ -103,9 +103,9 @@ def main():
     kalone = bench["roofline"].get("summing_kernel_alone")
     # launches per step: a batch of more than 1M frames runs as 1M-frame launches (config 4 on one GPU)
     # (the lane kernel, frames <= 128 B, takes up to 16M frames per launch)
-    per_step = -(-int(bench["config"]["frames_per_gpu"]) // (1 << (24 if int(bench["config"].get("frame_len") or 0) == 64 and
-                                                                       "lane" in bench["roofline"].get("kernels", "")
-                                                                       else 20)))
+    # (frame_len is a string for a mix: "imix")
+    lane64 = str(bench["config"].get("frame_len")) == "64" and "lane" in bench["roofline"].get("kernels", "")
+    per_step = -(-int(bench["config"]["frames_per_gpu"]) // (1 << (24 if lane64 else 20)))
     tail = per_step * (3 + int(bench.get("kernel_steps", 50))) if kalone else 0
     fetch = dispatches(d, "FETCH_SIZE")
     write = dispatches(d, "WRITE_SIZE")
