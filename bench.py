@@ -555,6 +555,7 @@ def c_host_multi_leg(args, dev, reps=10):
     mean = int(lens.mean())
     total = int(lens.astype(np.int64).sum())
     opts = [ChecksummerOptions(csum_iterations=i) for i in (1, 2)]
+    pristine = umem.clone()          # for one device's pass over the whole batch, the reference answer
     with multi.MultiDevice(range(ndev)) as m:
         scat = [m.scatter(0, umem.data_ptr(), umem.numel(), hd) for _ in range(3)]
         moved = sum(m.shard_info(k)["span_hi"] - m.shard_info(k)["span_lo"] + 16 * (m.shard_info(k)["frame_hi"] -
@@ -565,13 +566,36 @@ def c_host_multi_leg(args, dev, reps=10):
         m.process(opts[0], frame_len_max=1500, frame_len_mean=mean)   # the last pass -i 1
         cnt = m.counters()
         infos = [m.shard_info(k) for k in range(ndev)]
+        # out and back: the frames packed on the root (their bytes only), every
+        # device's records-only pass, the records applied to the root's UMEM
+        # (xsknf_gpu_multi_scatter_packed / _return); -i 1, so the root's UMEM
+        # and verdicts must equal one device's -i 1 pass over the whole batch
+        pk = [m.scatter_packed(0, umem.data_ptr(), umem.numel(), hd) for _ in range(3)]
+        pk_moved = sum(m.shard_info(k)["span_hi"] - m.shard_info(k)["span_lo"] for k in range(ndev)) + 16 * n
+        vret = torch.empty(n, dtype=torch.int32, device=dev)
+        rets = [m.return_results(umem.data_ptr(), vret.data_ptr(), opts[0], frame_len_max=1500, frame_len_mean=mean)
+                for _ in range(3)]
     # one device's pass over the whole batch, -i 1, and its counters on the device
     v = Checksummer(ChecksummerOptions(), num_interfaces=1, frame_len_hint=1500, frame_len_mean=mean).process_batch(
-        umem, dt)
-    fp = check_fingerprint(umem, dt, 0)
+        pristine, dt)
+    fp = check_fingerprint(pristine, dt, 0)
     single = {"frames": n, "bytes": total, "drop": int((v == -1).sum()), "forward": int((v >= 0).sum()),
               "checks_sum": fp[0], "checks_weighted": fp[1]}
-    del umem, dt, v
+    round_trip_match = bool(torch.equal(umem, pristine)) and bool(torch.equal(vret, v))
+    t_pk = sorted(pk)[1]
+    t_ret = sorted(r[1] for r in rets)[1]
+    pass_us = [round(sorted(r[0][k] for r in rets)[1] * 1e3, 2) for k in range(ndev)]
+    packed = {"scatter_ms": round(t_pk * 1e3, 3), "scatter_bytes": pk_moved,
+              "scatter_GBps": round(pk_moved / t_pk / 1e9, 1),
+              "return_ms": round(t_ret * 1e3, 3), "return_bytes": 4 * n,
+              "records_pass_us_per_device": pass_us,
+              "round_trip_ms": round((t_pk + t_ret) * 1e3, 3),
+              "match": round_trip_match,
+              "what": "frames packed into 16-byte slots on device 0 and sent (grouped ncclSend / ncclRecv); each "
+                      "device's records-only pass; 4 B per frame back; the checks applied to device 0's UMEM -- "
+                      "match: device 0's UMEM and verdicts equal one device's pass over the whole batch, every "
+                      "byte (medians of 3)"}
+    del umem, dt, v, pristine, vret
     per_dev = [sorted(st[k] for st in steps)[len(steps) // 2] for k in range(ndev)]
     step_max = sorted(max(st) for st in steps)[len(steps) // 2]
     t_scat = sorted(scat)[1]
@@ -584,7 +608,7 @@ def c_host_multi_leg(args, dev, reps=10):
             "step_us": round(step_max * 1e3, 2),
             "gbs_checksummed": round(total / (step_max / 1e3) / 1e9, 1),
             "mpps": round(n / (step_max / 1e3) / 1e6, 1),
-            "counters": cnt, "single_gpu": single, "match": cnt == single,
+            "counters": cnt, "single_gpu": single, "match": cnt == single, "packed_round_trip": packed,
             "api": "xsknf_gpu_multi_create (ncclCommInitAll) / _scatter (grouped ncclSend / ncclRecv from device "
                    "0) / _process (a stream per device) / _counters (ncclAllReduce); medians of "
                    f"{reps} steps, each the slowest device's HIP-event time"}

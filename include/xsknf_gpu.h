@@ -346,11 +346,14 @@ struct xsknf_gpu_multi;
  * weighted by ((global UMEM offset) mod 65521) + 1] */
 #define XSKNF_GPU_MULTI_COUNTERS 6
 
+#define XSKNF_GPU_SHARD_PACKED 1u   /* shard_info.flags: moved by xsknf_gpu_multi_scatter_packed */
+
 struct xsknf_gpu_shard_info {
 	int32_t device;          /* HIP device of the shard */
-	int32_t reserved;
+	uint32_t flags;          /* XSKNF_GPU_SHARD_PACKED */
 	uint64_t frame_lo, frame_hi;   /* frames [lo, hi) of the global batch */
-	uint64_t span_lo, span_hi;     /* its bytes [lo, hi) of the root's UMEM */
+	uint64_t span_lo, span_hi;     /* its bytes [lo, hi) of the root's UMEM (packed: of the root's
+	                                  packed buffer, the shard's own bytes starting at 0) */
 	uint64_t frame_bytes;          /* sum of its frame lengths */
 	uint8_t *umem;                 /* device buffers of the shard on its device */
 	struct xsknf_gpu_desc *descs;
@@ -374,8 +377,33 @@ XSKNF_GPU_API int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, c
 XSKNF_GPU_API int xsknf_gpu_multi_process(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex,
 		const struct xsknf_csum_opts *opts, uint32_t frame_len_max, uint32_t frame_len_mean, float *ms);
 /* The XSKNF_GPU_MULTI_COUNTERS counters of every shard, summed over the devices
- * by ncclAllReduce (the root's copy, to host memory). */
+ * by ncclAllReduce (the root's copy, to host memory).  -EOPNOTSUPP after a
+ * packed scatter (a packed shard no longer holds its frames' UMEM offsets,
+ * which the weighted sum needs; its results come back by _return). */
 XSKNF_GPU_API int xsknf_gpu_multi_counters(struct xsknf_gpu_multi *m, uint64_t *out);
+/* As xsknf_gpu_multi_scatter, moving only the frames' bytes: on the root a
+ * kernel copies each shard's frames into 16-byte aligned slots of a packed
+ * buffer (a frame keeps its address mod 16; the bytes that share its first and
+ * last 16-byte chunk travel with it), and each shard receives its packed bytes
+ * plus descriptors that address them (aligned-mode addresses; descriptors
+ * outside the UMEM keep their length and get an address past any span).  A
+ * UMEM of 2 KiB chunks holding IMIX frames moves ~1/5 of its span bytes.
+ * seconds (may be NULL): the packing and the moves. */
+XSKNF_GPU_API int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const uint8_t *umem,
+		uint64_t umem_size, const struct xsknf_gpu_desc *descs, uint64_t n, double *seconds);
+/* The whole batch's results back to the root, after either scatter: every
+ * device runs the summing pass over its shard in records-only mode (fused_stores
+ * 3: the shard is only read), sends its 4-byte record / verdict per frame to
+ * the root into verdicts[0..n) (device memory on the root, the scatter's frame
+ * order), and a kernel on the root writes each record's check into `umem` (the
+ * root UMEM the scatter read, at the frame the caller's descriptor names) and
+ * turns it into the forward verdict.  `umem` and `verdicts` then hold what one
+ * device's xsknf_gpu_checksum_batch over the whole batch leaves.  ms (may be
+ * NULL, ndev entries): each device's summing pass, HIP events; seconds (may be
+ * NULL): the whole return. */
+XSKNF_GPU_API int xsknf_gpu_multi_return(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex,
+		const struct xsknf_csum_opts *opts, uint32_t frame_len_max, uint32_t frame_len_mean, uint8_t *umem,
+		int32_t *verdicts, float *ms, double *seconds);
 XSKNF_GPU_API int xsknf_gpu_multi_shard_info(const struct xsknf_gpu_multi *m, int shard,
 		struct xsknf_gpu_shard_info *info);
 /* Copy shard `shard`'s UMEM span (span_hi - span_lo bytes), its rebased

@@ -162,6 +162,108 @@ def test_c_host_multi_device_cases(dev, case):
     _c_host_multi_run(dev, b.umem, b.descs, b.layout, action=action, nif=nif)
 
 
+def _c_host_packed_round_trip(dev, host, hd, action=0, nif=1, iters=1, mean=0):
+    """The global batch out and back through the C host's multi-device calls over
+    every visible device: xsknf_gpu_multi_scatter_packed (each shard's frames
+    packed into 16-byte slots on the root, then grouped ncclSend / ncclRecv),
+    xsknf_gpu_multi_return (each device's records-only pass, its records sent to
+    the root, applied there).  Checked: every shard holds exactly its frames'
+    bytes before the pass; afterwards the root's UMEM and verdicts equal the
+    reference's own pass over the whole batch, byte for byte."""
+    from xsknf_amd import ChecksummerOptions, _lib, multi
+    ndev = torch.cuda.device_count()
+    umem = torch.from_numpy(host).to(dev)
+    n = hd.shape[0]
+    v = torch.full((max(n, 1),), 0x7eadbeef, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    a = hd["addr"].astype(np.uint64)
+    off = ((a & np.uint64((1 << 48) - 1)) + (a >> np.uint64(48))).astype(np.int64)
+    ln = hd["len"].astype(np.int64)
+    inr = (off <= host.size) & (ln <= host.size - np.minimum(off, host.size))
+    rng = np.random.default_rng(n)
+    with multi.MultiDevice(range(ndev)) as m:
+        secs = m.scatter_packed(0, umem.data_ptr(), umem.numel(), hd)
+        moved = 0
+        for k in range(ndev):
+            info = m.shard_info(k)
+            assert info["flags"] == _lib.SHARD_PACKED and info["device"] == k
+            su, sv, sd = m.fetch(k, descs=True)
+            lo, hi = info["frame_lo"], info["frame_hi"]
+            moved += su.size
+            assert np.array_equal(sd["len"], hd["len"][lo:hi]) and np.array_equal(sd["options"], hd["options"][lo:hi])
+            idx = np.arange(lo, hi)
+            if idx.size > 3000:
+                idx = np.sort(rng.choice(idx, 3000, replace=False))
+            for f in idx:
+                if not inr[f]:
+                    assert sd["addr"][f - lo] >= su.size
+                    continue
+                p, L = int(sd["addr"][f - lo]), int(ln[f])
+                assert p % 16 == (umem.data_ptr() + int(off[f])) % 16
+                assert np.array_equal(su[p:p + L], host[off[f]:off[f] + L]), f"frame {f} packed bytes"
+        ms, secs2 = m.return_results(umem.data_ptr(), v.data_ptr(), ChecksummerOptions(action=action,
+                                                                                         csum_iterations=iters),
+                                     num_interfaces=nif, frame_len_max=int(hd["len"].max()) if n else 0,
+                                     frame_len_mean=mean)
+        with pytest.raises(_lib.XsknfGpuError):
+            m.counters()   # -EOPNOTSUPP after a packed scatter
+    ref = host.copy()
+    _, ov = oracles.time_batch(ref, hd, action=action, nif=nif, iters=iters)
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy()[:n], ov), "verdicts"
+    assert np.array_equal(umem.cpu().numpy(), ref), "root UMEM"
+    return secs, secs2, ms, moved
+
+
+@pytest.mark.slow
+def test_c_host_packed_round_trip_config4(dev):
+    """BASELINE config 4 (8,388,608 IMIX frames in 2 KiB chunks, 1 % edge cases)
+    out of the root packed and back as records: the root's UMEM and verdicts equal
+    the reference's pass over the whole batch, and the packed shards moved ~1/5
+    of the span bytes (the 2 KiB chunks' gaps stay home)."""
+    n = 8 << 20
+    b = frames.aligned_batch(n, "imix", seed=frames.SEED)
+    frames.inject_edge_cases(b, 0.01, seed=406)
+    secs, secs2, ms, moved = _c_host_packed_round_trip(dev, b.umem, b.descs, mean=int(b.descs["len"].mean()))
+    frame_bytes = int(b.descs["len"].astype(np.int64).sum())
+    assert frame_bytes <= moved < 1.1 * frame_bytes + 16 * n
+    print(f"c-host packed: moved {moved / 1e9:.2f} GB for {frame_bytes / 1e9:.2f} GB of frames "
+          f"(span {b.umem.size / 1e9:.1f} GB), scatter {secs * 1e3:.1f} ms, return {secs2 * 1e3:.1f} ms, pass {ms} ms")
+
+
+@pytest.mark.parametrize("case", ["unaligned-edges", "jumbo", "out-of-range", "drop-2if", "one-frame", "64B-iter3",
+                                  "ihl-overlap", "empty"])
+def test_c_host_packed_round_trip_cases(dev, case):
+    """Packed frames at odd addresses (unaligned UMEM, 10 % edge cases), jumbo
+    frames, descriptors outside the UMEM, DROP with two interfaces, one frame,
+    64-B frames (the lane kernel's records) with 3 iterations, frames whose UDP
+    header overlaps the IP header (ihl 2 / 3), an empty batch."""
+    action, nif, iters = 0, 1, 1
+    if case == "unaligned-edges":
+        b = frames.unaligned_batch(20000, "imix", seed=61)
+        frames.inject_edge_cases(b, 0.1, seed=62)
+    elif case == "jumbo":
+        b = frames.unaligned_batch(3000, 9000, seed=63)
+    elif case == "out-of-range":
+        b = frames.aligned_batch(5000, "imix", seed=64)
+        b.descs["addr"][::37] += np.uint64(1 << 40)
+    elif case == "drop-2if":
+        b = frames.aligned_batch(5000, 1500, seed=65)
+        action, nif = 1, 2
+    elif case == "one-frame":
+        b = frames.aligned_batch(1, 570, seed=66)
+    elif case == "64B-iter3":
+        b = frames.aligned_batch(30000, 64, seed=67)
+        iters = 3
+    elif case == "ihl-overlap":
+        b = frames.unaligned_batch(4000, "imix", seed=68)
+        frames.inject_edge_cases(b, 0.3, seed=69)
+    else:
+        b = frames.aligned_batch(1, 570, seed=70)
+        b = frames.HostBatch(b.umem, b.descs[:0].copy(), b.layout)
+    _c_host_packed_round_trip(dev, b.umem, b.descs, action=action, nif=nif, iters=iters)
+
+
 def _scatter_rank(rank, world, port, outdir):
     import torch
     import torch.distributed as dist

@@ -41,6 +41,8 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_shard_rebase",
     "xsknf_gpu_multi_create",
     "xsknf_gpu_multi_scatter",
+    "xsknf_gpu_multi_scatter_packed",
+    "xsknf_gpu_multi_return",
     "xsknf_gpu_multi_process",
     "xsknf_gpu_multi_counters",
     "xsknf_gpu_multi_shard_info",
@@ -92,10 +94,13 @@ class CtxStats(ctypes.Structure):
                 ("resident_batches", ctypes.c_uint64), ("resident_launches", ctypes.c_uint64)]
 
 
+SHARD_PACKED = 1   # XSKNF_GPU_SHARD_PACKED
+
+
 class ShardInfo(ctypes.Structure):
     """struct xsknf_gpu_shard_info (include/xsknf_gpu.h)."""
 
-    _fields_ = [("device", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("frame_lo", ctypes.c_uint64), ("frame_hi", ctypes.c_uint64),
                 ("span_lo", ctypes.c_uint64), ("span_hi", ctypes.c_uint64),
                 ("frame_bytes", ctypes.c_uint64),
@@ -213,6 +218,11 @@ def load() -> ctypes.CDLL:
     lib.xsknf_gpu_multi_scatter.restype = ctypes.c_int
     lib.xsknf_gpu_multi_scatter.argtypes = [vp, ctypes.c_int, vp, u64, vp, u64, ctypes.POINTER(ctypes.c_double)]
     lib.xsknf_gpu_multi_process.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_scatter_packed.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_scatter_packed.argtypes = [vp, ctypes.c_int, vp, u64, vp, u64, ctypes.POINTER(ctypes.c_double)]
+    lib.xsknf_gpu_multi_return.restype = ctypes.c_int
+    lib.xsknf_gpu_multi_return.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(CsumOpts), ctypes.c_uint32,
+                                           ctypes.c_uint32, vp, vp, vp, ctypes.POINTER(ctypes.c_double)]
     lib.xsknf_gpu_multi_process.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(CsumOpts), ctypes.c_uint32,
                                             ctypes.c_uint32, vp]
     lib.xsknf_gpu_multi_counters.restype = ctypes.c_int

@@ -23,6 +23,18 @@
 //     written checks, the same weighted by global UMEM offset} per device,
 //     summed over devices by ncclAllReduce: the whole batch's result, as one
 //     device's pass over all of it would give it.
+//   * xsknf_gpu_multi_scatter_packed -- the same distribution moving only the
+//     frames' bytes: a gather kernel on the root copies each shard's frames
+//     into 16-byte slots (a frame keeps its address mod 16), so a UMEM of 2 KiB
+//     chunks holding IMIX frames (mean 352 B) sends ~1/5 of its span bytes.
+//   * xsknf_gpu_multi_return -- the results back to the root: each device runs
+//     the summing pass in records-only mode over its shard (include/
+//     xsknf_gpu.h fused_stores 3: the shard is only read), sends its 4-byte
+//     records / verdicts to the root (grouped ncclSend / ncclRecv), and an apply
+//     kernel on the root writes every changed check into the root's UMEM and
+//     every final verdict: the root ends with the bytes and verdicts of one
+//     device's pass over the whole batch, having moved frames out and 4 bytes
+//     per frame back.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <errno.h>
@@ -117,6 +129,81 @@ __global__ void __launch_bounds__(256) shard_counters(const uint8_t *umem, uint6
   }
 }
 
+// Root: copy frames [0, n) of one shard into its packed buffer.  Frame f's
+// bytes lie in the 16-byte aligned chunks [src & ~15, round16(src + len)) of
+// memory (src = its address) and go to the slot at dst & ~15 of the packed
+// buffer, whose length is exactly those chunks (dst = src mod 16 + the slot's
+// start): whole chunks move, and the bytes around the frame in its first and
+// last chunk are copied with it into its own slot.  One wave per 64 frames:
+// the tile's chunk counts are prefix-summed across the wave and the lanes deal
+// the tile's chunks round robin (a 64-B frame is 4-5 chunks, a jumbo one 563).
+// A chunk reaching past the UMEM's end is copied byte by byte.
+__global__ void __launch_bounds__(256) pack_frames(const uint8_t *umem, uint64_t umem_size,
+                                                   const xsknf_gpu_desc *orig, const xsknf_gpu_desc *packed,
+                                                   uint64_t n, uint8_t *dst) {
+  __shared__ uint32_t pre[4][65];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t tiles = (n + 63) / 64;
+  for (uint64_t t = blockIdx.x * 4ull + wv; t < tiles; t += gridDim.x * 4ull) {
+    const uint64_t f = t * 64 + lane;
+    uint64_t s0 = 0, d0 = 0;   // the first chunk's address (absolute) and its slot offset in dst
+    uint32_t nch = 0;
+    if (f < n) {
+      const xsknf_gpu_desc o = orig[f], q = packed[f];
+      const uint64_t src = reinterpret_cast<uintptr_t>(umem) + umem_offset(o.addr);
+      if (q.addr != kOutOfRange && o.len > 0) {
+        s0 = src & ~15ull;
+        d0 = q.addr & ~15ull;
+        nch = static_cast<uint32_t>(((src & 15) + o.len + 15) >> 4);
+      }
+    }
+    // inclusive scan of the chunk counts over the wave
+    uint32_t x = nch;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    pre[wv][lane + 1] = x;
+    if (lane == 0) pre[wv][0] = 0;
+    __builtin_amdgcn_wave_barrier();   // (one wave's LDS accesses complete in order)
+    const uint32_t total = __shfl(x, 63);
+    const uint64_t begin = reinterpret_cast<uintptr_t>(umem), end = begin + umem_size;
+    for (uint32_t k = lane; k < total; k += 64) {
+      // the frame j of the tile whose chunks hold chunk k: pre[j] <= k < pre[j + 1]
+      int lo = 0, hi = 63;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[wv][mid] <= k) lo = mid; else hi = mid - 1;
+      }
+      const uint32_t c = k - pre[wv][lo];
+      const uint64_t sa = __shfl(s0, lo) + 16ull * c, da = __shfl(d0, lo) + 16ull * c;
+      if (sa >= begin && sa + 16 <= end) {
+        *reinterpret_cast<uint4 *>(dst + da) = *reinterpret_cast<const uint4 *>(sa);
+      } else {   // a chunk reaching before the UMEM's first byte or past its last
+        for (uint64_t b = sa > begin ? sa : begin; b < sa + 16 && b < end; ++b)
+          dst[da + (b - sa)] = *reinterpret_cast<const uint8_t *>(b);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();   // pre[wv] is rewritten by the next tile
+  }
+}
+
+// Root: the returned records / verdicts of the whole batch, in place: a record
+// (XSKNF_GPU_RECORD_TAG | u << 16 | check) writes the check's two bytes, low
+// byte first, at the frame's offset u + 6 (checksummer_user.c:108) and becomes
+// the forward verdict (:110-111); any other value is already the verdict.
+__global__ void __launch_bounds__(256) apply_records(uint8_t *umem, const xsknf_gpu_desc *orig, int32_t *verdicts,
+                                                     uint64_t n, int32_t fwd) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    const uint32_t r = static_cast<uint32_t>(verdicts[i]);
+    if ((r & XSKNF_GPU_RECORD_TAG_MASK) != XSKNF_GPU_RECORD_TAG) continue;
+    uint8_t *p = umem + umem_offset(orig[i].addr) + ((r >> 16) & 0x7f) + 6;
+    p[0] = static_cast<uint8_t>(r);
+    p[1] = static_cast<uint8_t>(r >> 8);
+    verdicts[i] = fwd;
+  }
+}
+
 struct Shard {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -130,6 +217,7 @@ struct Shard {
   int32_t *verdicts = nullptr;
   uint64_t frames_cap = 0;
   unsigned long long *counters = nullptr;   // device: XSKNF_GPU_MULTI_COUNTERS
+  uint64_t pack_lo = 0;          // packed scatter: the shard's bytes [pack_lo, pack_lo + b1 - b0) of the root's packed buffer
 };
 
 }  // namespace
@@ -144,7 +232,115 @@ struct xsknf_gpu_multi {
   int root_descs_dev = -1;                // the device root_descs lives on
   int root = -1;                          // index of the root of the last scatter
   uint64_t n = 0;                         // frames of the last scatter
+  bool packed = false;                    // the last scatter moved packed frames
+  // on the root device (root_descs_dev): the last scatter's descriptors as the
+  // caller gave them (for the results' return) and the packed staging buffer
+  xsknf_gpu_desc *root_orig = nullptr;
+  uint64_t root_orig_cap = 0;
+  uint8_t *root_pack = nullptr;
+  uint64_t root_pack_cap = 0;
 };
+
+namespace {
+
+// (Re)allocate a root-device buffer to at least `bytes`.
+template <typename T>
+hipError_t root_buffer(T *&p, uint64_t &cap, uint64_t bytes) {
+  if (p && bytes <= cap) return hipSuccess;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes ? bytes : 1);
+  if (e == hipSuccess) cap = bytes;
+  return e;
+}
+
+// The root-side staging of a scatter: the device the root buffers live on
+// becomes devices[root] (buffers of an earlier root are freed), the caller's
+// descriptors go to root_orig (for the results' return) and `sent` (the
+// descriptors each shard receives, in global order) to root_descs.
+hipError_t stage_root(xsknf_gpu_multi *m, int root, const xsknf_gpu_desc *descs, const xsknf_gpu_desc *sent,
+                      uint64_t n) {
+  hipError_t e = hipSuccess;
+  if (m->root_descs_dev >= 0 && m->root_descs_dev != m->devices[root]) {
+    e = hipSetDevice(m->root_descs_dev);
+    for (void *p : {static_cast<void *>(m->root_descs), static_cast<void *>(m->root_orig),
+                    static_cast<void *>(m->root_pack)})
+      if (e == hipSuccess && p) e = hipFree(p);
+    m->root_descs = m->root_orig = nullptr;
+    m->root_pack = nullptr;
+    m->root_descs_cap = m->root_orig_cap = m->root_pack_cap = 0;
+  }
+  if (e == hipSuccess) e = hipSetDevice(m->devices[root]);
+  m->root_descs_dev = m->devices[root];
+  const uint64_t bytes = sizeof(xsknf_gpu_desc) * n;
+  uint64_t cap_d = m->root_descs_cap * sizeof(xsknf_gpu_desc), cap_o = m->root_orig_cap * sizeof(xsknf_gpu_desc);
+  if (e == hipSuccess) e = root_buffer(m->root_descs, cap_d, bytes);
+  if (e == hipSuccess) e = root_buffer(m->root_orig, cap_o, bytes);
+  m->root_descs_cap = cap_d / sizeof(xsknf_gpu_desc);
+  m->root_orig_cap = cap_o / sizeof(xsknf_gpu_desc);
+  if (e == hipSuccess && n) e = hipMemcpy(m->root_descs, sent, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) e = hipMemcpy(m->root_orig, descs, bytes, hipMemcpyHostToDevice);
+  return e;
+}
+
+// A shard's device buffers for `span` bytes (+ 16 spare: the kernels' 16-byte
+// chunk loads) and `frames` descriptors / verdicts; the spare bytes zeroed.
+hipError_t shard_buffers(Shard &s, uint64_t span, uint64_t frames) {
+  hipError_t e = hipSetDevice(s.device);
+  const uint64_t need = span + 16;
+  if (e == hipSuccess && need > s.umem_cap) {
+    if (s.umem) (void)hipFree(s.umem);
+    s.umem = nullptr;
+    s.umem_cap = 0;
+    e = hipMalloc(&s.umem, need);
+    if (e == hipSuccess) s.umem_cap = need;
+  }
+  if (e == hipSuccess && frames > s.frames_cap) {
+    if (s.descs) (void)hipFree(s.descs);
+    if (s.verdicts) (void)hipFree(s.verdicts);
+    s.descs = nullptr;
+    s.verdicts = nullptr;
+    s.frames_cap = 0;
+    e = hipMalloc(&s.descs, sizeof(xsknf_gpu_desc) * (frames ? frames : 1));
+    if (e == hipSuccess) e = hipMalloc(&s.verdicts, sizeof(int32_t) * (frames ? frames : 1));
+    if (e == hipSuccess) s.frames_cap = frames;
+  }
+  if (e == hipSuccess) e = hipMemsetAsync(s.umem + span, 0, 16, s.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+  return e;
+}
+
+// One grouped set of point-to-point moves, in kP2PPiece pieces: each
+// (src on devices[from], dst on devices[to], bytes) as ncclSend on `from`'s
+// communicator / stream and ncclRecv on `to`'s.
+struct Move {
+  const uint8_t *src;
+  uint8_t *dst;
+  uint64_t bytes;
+  int from, to;
+};
+
+int grouped_moves(xsknf_gpu_multi *m, const std::vector<Move> &moves, const char *what) {
+  ncclResult_t r = ncclGroupStart();
+  for (const Move &mv : moves)
+    for (uint64_t o = 0; o < mv.bytes && r == ncclSuccess; o += kP2PPiece) {
+      const size_t len = mv.bytes - o < kP2PPiece ? mv.bytes - o : kP2PPiece;
+      r = ncclSend(mv.src + o, len, ncclUint8, mv.to, m->comms[mv.from], m->sh[mv.from].stream);
+      if (r == ncclSuccess) r = ncclRecv(mv.dst + o, len, ncclUint8, mv.from, m->comms[mv.to], m->sh[mv.to].stream);
+    }
+  const ncclResult_t r2 = ncclGroupEnd();
+  if (r != ncclSuccess) return nccl_fail(r, what);
+  if (r2 != ncclSuccess) return nccl_fail(r2, what);
+  for (Shard &s : m->sh) {
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) return hip_fail(e, what);
+  }
+  return 0;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -254,23 +450,7 @@ int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, const uint8_t *
   for (int k = 0; k < N; ++k)
     xsknf_gpu_shard_rebase(descs + bounds[k], bounds[k + 1] - bounds[k], spans[2 * k], umem_size,
                            rebased.data() + bounds[k]);
-  hipError_t e = hipSuccess;
-  if (m->root_descs && (n > m->root_descs_cap || m->root_descs_dev != m->devices[root])) {
-    e = hipSetDevice(m->root_descs_dev);
-    if (e == hipSuccess) e = hipFree(m->root_descs);
-    m->root_descs = nullptr;
-    m->root_descs_cap = 0;
-  }
-  if (e == hipSuccess) e = hipSetDevice(m->devices[root]);
-  if (e == hipSuccess && !m->root_descs && n) {
-    e = hipMalloc(&m->root_descs, sizeof(xsknf_gpu_desc) * n);
-    if (e == hipSuccess) {
-      m->root_descs_cap = n;
-      m->root_descs_dev = m->devices[root];
-    }
-  }
-  if (e == hipSuccess && n)
-    e = hipMemcpy(m->root_descs, rebased.data(), sizeof(xsknf_gpu_desc) * n, hipMemcpyHostToDevice);
+  hipError_t e = stage_root(m, root, descs, rebased.data(), n);
   if (e != hipSuccess) return hip_fail(e, "multi scatter: root descriptors");
   for (int k = 0; k < N; ++k) {
     Shard &s = m->sh[k];
@@ -278,63 +458,106 @@ int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, const uint8_t *
     s.hi = bounds[k + 1];
     s.b0 = spans[2 * k];
     s.b1 = spans[2 * k + 1];
+    s.pack_lo = 0;
     s.bytes = 0;
     for (uint64_t f = s.lo; f < s.hi; ++f) s.bytes += descs[f].len;
-    e = hipSetDevice(s.device);
-    const uint64_t need = s.b1 - s.b0 + 16, frames = s.hi - s.lo;
-    if (e == hipSuccess && need > s.umem_cap) {
-      if (s.umem) (void)hipFree(s.umem);
-      s.umem = nullptr;
-      s.umem_cap = 0;
-      e = hipMalloc(&s.umem, need);
-      if (e == hipSuccess) s.umem_cap = need;
-    }
-    if (e == hipSuccess && frames > s.frames_cap) {
-      if (s.descs) (void)hipFree(s.descs);
-      if (s.verdicts) (void)hipFree(s.verdicts);
-      s.descs = nullptr;
-      s.verdicts = nullptr;
-      s.frames_cap = 0;
-      e = hipMalloc(&s.descs, sizeof(xsknf_gpu_desc) * frames);
-      if (e == hipSuccess) e = hipMalloc(&s.verdicts, sizeof(int32_t) * frames);
-      if (e == hipSuccess) s.frames_cap = frames;
-    }
-    // the spare bytes past the span: defined (the loads that reach them are masked)
-    if (e == hipSuccess) e = hipMemsetAsync(s.umem + (s.b1 - s.b0), 0, 16, s.stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    e = shard_buffers(s, s.b1 - s.b0, s.hi - s.lo);
     if (e != hipSuccess) return hip_fail(e, "multi scatter: shard buffers");
   }
   // every shard at once: the root sends each its span and descriptors, every
-  // device receives its own (the root's to itself), one group, in pieces of
-  // kP2PPiece bytes
-  const uint64_t piece = kP2PPiece;
+  // device receives its own (the root's to itself), one group
   const double t0 = now_s();
-  Shard &rs = m->sh[root];
-  ncclResult_t r = ncclGroupStart();
-  const auto pair = [&](const uint8_t *src, uint8_t *dst, uint64_t bytes, int k) {
-    for (uint64_t o = 0; o < bytes && r == ncclSuccess; o += piece) {
-      const size_t len = bytes - o < piece ? bytes - o : piece;
-      r = ncclSend(src + o, len, ncclUint8, k, m->comms[root], rs.stream);
-      if (r == ncclSuccess) r = ncclRecv(dst + o, len, ncclUint8, root, m->comms[k], m->sh[k].stream);
-    }
-  };
-  for (int k = 0; k < N && r == ncclSuccess; ++k) {
+  std::vector<Move> moves;
+  for (int k = 0; k < N; ++k) {
     Shard &s = m->sh[k];
-    pair(umem + s.b0, s.umem, s.b1 - s.b0, k);
-    pair(reinterpret_cast<const uint8_t *>(m->root_descs + s.lo), reinterpret_cast<uint8_t *>(s.descs),
-         sizeof(xsknf_gpu_desc) * (s.hi - s.lo), k);
+    moves.push_back({umem + s.b0, s.umem, s.b1 - s.b0, root, k});
+    moves.push_back({reinterpret_cast<const uint8_t *>(m->root_descs + s.lo), reinterpret_cast<uint8_t *>(s.descs),
+                     sizeof(xsknf_gpu_desc) * (s.hi - s.lo), root, k});
   }
-  const ncclResult_t r2 = ncclGroupEnd();
-  if (r != ncclSuccess) return nccl_fail(r, "multi scatter: ncclSend / ncclRecv");
-  if (r2 != ncclSuccess) return nccl_fail(r2, "multi scatter: ncclGroupEnd");
-  for (Shard &s : m->sh) {
-    e = hipSetDevice(s.device);
-    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
-    if (e != hipSuccess) return hip_fail(e, "multi scatter: wait");
-  }
+  rc = grouped_moves(m, moves, "multi scatter: ncclSend / ncclRecv");
+  if (rc) return rc;
   if (seconds) *seconds = now_s() - t0;
   m->root = root;
   m->n = n;
+  m->packed = false;
+  return 0;
+}
+
+int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const uint8_t *umem, uint64_t umem_size,
+                                   const struct xsknf_gpu_desc *descs, uint64_t n, double *seconds) {
+  if (!m || root < 0 || root >= m->ndev || (n && (!umem || !descs))) return -EINVAL;
+  const int N = m->ndev;
+  std::vector<uint64_t> bounds(N + 1);
+  int rc = xsknf_gpu_shard_plan(descs, n, umem_size, static_cast<uint32_t>(N), bounds.data(), nullptr);
+  if (rc) return rc;
+  // the packed layout: shard k's frames in global order, each in its own
+  // 16-byte aligned slot at the same address mod 16 as in the UMEM; the
+  // descriptors each shard receives address its own packed bytes
+  std::vector<xsknf_gpu_desc> packed(n);
+  std::vector<uint64_t> pk_lo(N), pk_size(N);
+  const uintptr_t ubase = reinterpret_cast<uintptr_t>(umem);
+  uint64_t total = 0;
+  for (int k = 0; k < N; ++k) {
+    uint64_t pos = 0;
+    for (uint64_t f = bounds[k]; f < bounds[k + 1]; ++f) {
+      const xsknf_gpu_desc d = descs[f];
+      packed[f].len = d.len;
+      packed[f].options = d.options;
+      if (!in_umem(d, umem_size)) {
+        packed[f].addr = kOutOfRange;
+        continue;
+      }
+      const uint64_t rs = (ubase + umem_offset(d.addr)) & 15;
+      packed[f].addr = pos + rs;
+      pos += d.len ? (rs + d.len + 15) & ~15ull : 0;
+    }
+    pk_lo[k] = total;
+    pk_size[k] = pos;
+    total += pos;
+  }
+  hipError_t e = stage_root(m, root, descs, packed.data(), n);
+  if (e == hipSuccess) e = root_buffer(m->root_pack, m->root_pack_cap, total);
+  if (e != hipSuccess) return hip_fail(e, "multi packed scatter: root buffers");
+  for (int k = 0; k < N; ++k) {
+    Shard &s = m->sh[k];
+    s.lo = bounds[k];
+    s.hi = bounds[k + 1];
+    s.b0 = 0;
+    s.b1 = pk_size[k];
+    s.pack_lo = pk_lo[k];
+    s.bytes = 0;
+    for (uint64_t f = s.lo; f < s.hi; ++f) s.bytes += descs[f].len;
+    e = shard_buffers(s, pk_size[k], s.hi - s.lo);
+    if (e != hipSuccess) return hip_fail(e, "multi packed scatter: shard buffers");
+  }
+  const double t0 = now_s();
+  // gather every shard's frames on the root, on the root's stream (its sends
+  // follow on the same stream)
+  Shard &rs = m->sh[root];
+  e = hipSetDevice(rs.device);
+  for (int k = 0; k < N && e == hipSuccess; ++k) {
+    const uint64_t frames = bounds[k + 1] - bounds[k];
+    if (!frames) continue;
+    const uint64_t want = (frames + 255) / 256;
+    const unsigned grid = static_cast<unsigned>(want < 4096 ? want : 4096);
+    hipLaunchKernelGGL(pack_frames, dim3(grid), dim3(256), 0, rs.stream, umem, umem_size, m->root_orig + bounds[k],
+                       m->root_descs + bounds[k], frames, m->root_pack + pk_lo[k]);
+    e = hipGetLastError();
+  }
+  if (e != hipSuccess) return hip_fail(e, "multi packed scatter: pack_frames");
+  std::vector<Move> moves;
+  for (int k = 0; k < N; ++k) {
+    Shard &s = m->sh[k];
+    moves.push_back({m->root_pack + pk_lo[k], s.umem, pk_size[k], root, k});
+    moves.push_back({reinterpret_cast<const uint8_t *>(m->root_descs + s.lo), reinterpret_cast<uint8_t *>(s.descs),
+                     sizeof(xsknf_gpu_desc) * (s.hi - s.lo), root, k});
+  }
+  rc = grouped_moves(m, moves, "multi packed scatter: ncclSend / ncclRecv");
+  if (rc) return rc;
+  if (seconds) *seconds = now_s() - t0;
+  m->root = root;
+  m->n = n;
+  m->packed = true;
   return 0;
 }
 
@@ -369,6 +592,10 @@ int xsknf_gpu_multi_process(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex,
 
 int xsknf_gpu_multi_counters(struct xsknf_gpu_multi *m, uint64_t *out) {
   if (!m || !out || m->root < 0) return -EINVAL;
+  // the weighted check sum needs each frame's place in the root's UMEM, which
+  // a packed shard no longer holds: after a packed scatter the results come
+  // back whole (xsknf_gpu_multi_return) and are checked there
+  if (m->packed) return -EOPNOTSUPP;
   for (Shard &s : m->sh) {
     hipError_t e = hipSetDevice(s.device);
     if (e == hipSuccess)
@@ -403,15 +630,67 @@ int xsknf_gpu_multi_counters(struct xsknf_gpu_multi *m, uint64_t *out) {
   return e == hipSuccess ? 0 : hip_fail(e, "multi counters: copy");
 }
 
+int xsknf_gpu_multi_return(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex, const struct xsknf_csum_opts *opts,
+                           uint32_t frame_len_max, uint32_t frame_len_mean, uint8_t *umem, int32_t *verdicts, float *ms,
+                           double *seconds) {
+  if (!m || !opts || m->root < 0 || (m->n && (!umem || !verdicts))) return -EINVAL;
+  xsknf_gpu_launch_cfg cfg;
+  int rc = xsknf_gpu_launch_cfg_for_lens(frame_len_max, frame_len_mean, &cfg);
+  if (rc) return rc;
+  cfg.fused_stores = 3;   // records only: the shard is read, each changed check comes back as a record
+  const double t0 = now_s();
+  for (Shard &s : m->sh) {
+    const uint64_t frames = s.hi - s.lo;
+    if (frames > UINT32_MAX) return -EINVAL;
+    hipError_t e = hipSetDevice(s.device);
+    if (e == hipSuccess) e = hipEventRecord(s.e0, s.stream);
+    if (e != hipSuccess) return hip_fail(e, "multi return: start");
+    rc = xsknf_gpu_checksum_batch_cfg(s.umem, s.b1 - s.b0, s.descs, static_cast<uint32_t>(frames), ingress_ifindex,
+                                      opts, s.verdicts, &cfg, s.stream);
+    if (rc) return rc;
+    e = hipEventRecord(s.e1, s.stream);
+    if (e != hipSuccess) return hip_fail(e, "multi return: end");
+  }
+  // every device's records to the root, into the caller's verdict array, one group
+  std::vector<Move> moves;
+  for (int k = 0; k < m->ndev; ++k) {
+    Shard &s = m->sh[k];
+    moves.push_back({reinterpret_cast<const uint8_t *>(s.verdicts), reinterpret_cast<uint8_t *>(verdicts + s.lo),
+                     sizeof(int32_t) * (s.hi - s.lo), k, m->root});
+  }
+  rc = grouped_moves(m, moves, "multi return: ncclSend / ncclRecv");
+  if (rc) return rc;
+  for (int k = 0; k < m->ndev && ms; ++k) {
+    hipError_t e = hipSetDevice(m->sh[k].device);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms[k], m->sh[k].e0, m->sh[k].e1);
+    if (e != hipSuccess) return hip_fail(e, "multi return: events");
+  }
+  // the root applies them to its UMEM, with the descriptors the caller scattered
+  Shard &rs = m->sh[m->root];
+  hipError_t e = hipSetDevice(rs.device);
+  if (e == hipSuccess && m->n) {
+    const int32_t fwd = opts->action == XSKNF_CSUM_ACTION_REDIRECT
+                            ? static_cast<int32_t>((ingress_ifindex + 1u) % opts->num_interfaces) : -1;
+    const uint64_t want = (m->n + 255) / 256;
+    const unsigned grid = static_cast<unsigned>(want < 4096 ? want : 4096);
+    hipLaunchKernelGGL(apply_records, dim3(grid), dim3(256), 0, rs.stream, umem, m->root_orig, verdicts, m->n, fwd);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(rs.stream);
+  }
+  if (e != hipSuccess) return hip_fail(e, "multi return: apply_records");
+  if (seconds) *seconds = now_s() - t0;
+  return 0;
+}
+
 int xsknf_gpu_multi_shard_info(const struct xsknf_gpu_multi *m, int k, struct xsknf_gpu_shard_info *info) {
   if (!m || !info || k < 0 || k >= m->ndev) return -EINVAL;
   const Shard &s = m->sh[k];
   info->device = s.device;
-  info->reserved = 0;
+  info->flags = m->packed ? XSKNF_GPU_SHARD_PACKED : 0;
   info->frame_lo = s.lo;
   info->frame_hi = s.hi;
-  info->span_lo = s.b0;
-  info->span_hi = s.b1;
+  info->span_lo = m->packed ? s.pack_lo : s.b0;
+  info->span_hi = m->packed ? s.pack_lo + s.b1 : s.b1;
   info->frame_bytes = s.bytes;
   info->umem = s.umem;
   info->descs = s.descs;
@@ -446,7 +725,11 @@ int xsknf_gpu_multi_destroy(struct xsknf_gpu_multi *m) {
     if (s.e1) (void)hipEventDestroy(s.e1);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
-  if (m->root_descs && hipSetDevice(m->root_descs_dev) == hipSuccess) (void)hipFree(m->root_descs);
+  if (m->root_descs_dev >= 0 && hipSetDevice(m->root_descs_dev) == hipSuccess) {
+    if (m->root_descs) (void)hipFree(m->root_descs);
+    if (m->root_orig) (void)hipFree(m->root_orig);
+    if (m->root_pack) (void)hipFree(m->root_pack);
+  }
   for (ncclComm_t c : m->comms)
     if (c) (void)ncclCommDestroy(c);
   delete m;

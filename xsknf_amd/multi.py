@@ -85,6 +85,33 @@ class MultiDevice:
                                                      ctypes.byref(secs)), "xsknf_gpu_multi_scatter")
         return secs.value
 
+    def scatter_packed(self, root: int, umem_ptr: int, umem_size: int, descs) -> float:
+        """As scatter(), moving only the frames' bytes (xsknf_gpu_multi_scatter_packed:
+        packed into 16-byte slots on the root first); seconds."""
+        d = _descs_array(descs)
+        secs = ctypes.c_double()
+        _lib.check(self._lib.xsknf_gpu_multi_scatter_packed(self._h, root, ctypes.c_void_p(umem_ptr), umem_size,
+                                                            d.ctypes.data if d.shape[0] else None,
+                                                            int(d.shape[0]), ctypes.byref(secs)),
+                   "xsknf_gpu_multi_scatter_packed")
+        return secs.value
+
+    def return_results(self, umem_ptr: int, verdicts_ptr: int, opts: ChecksummerOptions | None = None,
+                       num_interfaces: int = 1, ingress_ifindex: int = 0, frame_len_max: int = 0,
+                       frame_len_mean: int = 0):
+        """xsknf_gpu_multi_return: every shard's results (records-only pass) back to
+        the root's UMEM at umem_ptr and int32 verdicts at verdicts_ptr (device
+        pointers on the root); (each device's milliseconds, seconds in all)."""
+        o = opts or ChecksummerOptions()
+        c = _lib.CsumOpts(o.csum_iterations, o.action, num_interfaces, 0)
+        ms = (ctypes.c_float * len(self.devices))()
+        secs = ctypes.c_double()
+        _lib.check(self._lib.xsknf_gpu_multi_return(self._h, ingress_ifindex, ctypes.byref(c), frame_len_max,
+                                                    frame_len_mean, ctypes.c_void_p(umem_ptr),
+                                                    ctypes.c_void_p(verdicts_ptr), ms, ctypes.byref(secs)),
+                   "xsknf_gpu_multi_return")
+        return list(ms), secs.value
+
     def process(self, opts: ChecksummerOptions | None = None, num_interfaces: int = 1, ingress_ifindex: int = 0,
                 frame_len_max: int = 0, frame_len_mean: int = 0):
         """Checksum every shard; returns each device's milliseconds."""
