@@ -142,6 +142,7 @@ __global__ void __launch_bounds__(256) pack_frames(const uint8_t *umem, uint64_t
                                                    const xsknf_gpu_desc *orig, const xsknf_gpu_desc *packed,
                                                    uint64_t n, uint8_t *dst) {
   __shared__ uint32_t pre[4][65];
+  __shared__ uint64_t src_of[4][64], dst_of[4][64];   // a frame's first chunk and its slot (read by any lane)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t tiles = (n + 63) / 64;
   for (uint64_t t = blockIdx.x * 4ull + wv; t < tiles; t += gridDim.x * 4ull) {
@@ -165,6 +166,8 @@ __global__ void __launch_bounds__(256) pack_frames(const uint8_t *umem, uint64_t
     }
     pre[wv][lane + 1] = x;
     if (lane == 0) pre[wv][0] = 0;
+    src_of[wv][lane] = s0;
+    dst_of[wv][lane] = d0;
     __builtin_amdgcn_wave_barrier();   // (one wave's LDS accesses complete in order)
     const uint32_t total = __shfl(x, 63);
     const uint64_t begin = reinterpret_cast<uintptr_t>(umem), end = begin + umem_size;
@@ -176,7 +179,9 @@ __global__ void __launch_bounds__(256) pack_frames(const uint8_t *umem, uint64_t
         if (pre[wv][mid] <= k) lo = mid; else hi = mid - 1;
       }
       const uint32_t c = k - pre[wv][lo];
-      const uint64_t sa = __shfl(s0, lo) + 16ull * c, da = __shfl(d0, lo) + 16ull * c;
+      // (from LDS, not by a lane shuffle: the loop's last round leaves lanes
+      // inactive, and a shuffle reads nothing from an inactive lane)
+      const uint64_t sa = src_of[wv][lo] + 16ull * c, da = dst_of[wv][lo] + 16ull * c;
       if (sa >= begin && sa + 16 <= end) {
         *reinterpret_cast<uint4 *>(dst + da) = *reinterpret_cast<const uint4 *>(sa);
       } else {   // a chunk reaching before the UMEM's first byte or past its last
