@@ -360,6 +360,16 @@ struct xsknf_gpu_shard_info {
 	int32_t *verdicts;
 };
 
+/* The packed layout of xsknf_gpu_multi_scatter_packed (no GPU): for shards
+ * [bounds[k], bounds[k+1]) of n descriptors over a UMEM at device address
+ * umem_addr, each frame gets a 16-byte aligned slot in its shard's packed
+ * buffer, at the same address mod 16 as in the UMEM; packed[f] is frame f's
+ * descriptor there (its length and options kept; a descriptor outside the
+ * UMEM gets an address past any span and no slot), sizes[k] shard k's packed
+ * bytes.  A frame of len bytes at address a mod 16 = r takes round16(r + len). */
+XSKNF_GPU_API int xsknf_gpu_shard_pack_plan(const struct xsknf_gpu_desc *descs, uint64_t n, uint64_t umem_addr,
+		uint64_t umem_size, uint32_t nshards, const uint64_t *bounds, struct xsknf_gpu_desc *packed,
+		uint64_t *sizes);
 /* One RCCL communicator per device of devices[0..ndev) (NULL: devices 0..ndev-1,
  * each at most once), a stream each. */
 XSKNF_GPU_API int xsknf_gpu_multi_create(struct xsknf_gpu_multi **m, const int *devices, int ndev);

@@ -214,3 +214,50 @@ def test_c_shard_plan_edges():
     d["addr"] = np.arange(lens.shape[0], dtype=np.uint64) * np.uint64(2048) + np.uint64(256)
     r, _ = multi.shard_plan(d, 8, lens.shape[0] * 2048)
     assert r == shard_by_bytes(lens, 8)
+
+
+def _pack_plan_py(descs, bounds, umem_addr, umem_size):
+    """The packed layout restated in numpy (include/xsknf_gpu.h
+    xsknf_gpu_shard_pack_plan): each in-UMEM frame of a shard, in order, in a
+    16-byte aligned slot of round16(r + len) bytes at address mod 16 = r, its
+    address within the shard's buffer = the slot's start + r."""
+    from xsknf_amd.shard import OUT_OF_RANGE, _in_umem, effective_offsets
+    out = np.zeros_like(descs)
+    out["len"], out["options"] = descs["len"], descs["options"]
+    inr = _in_umem(descs, umem_size)
+    r = ((np.uint64(umem_addr) + effective_offsets(descs).astype(np.uint64)) & np.uint64(15)).astype(np.int64)
+    ln = descs["len"].astype(np.int64)
+    slot = np.where(inr & (ln > 0), (r + ln + 15) // 16 * 16, 0)
+    sizes = []
+    for k in range(len(bounds) - 1):
+        lo, hi = bounds[k], bounds[k + 1]
+        start = np.concatenate([[0], np.cumsum(slot[lo:hi])[:-1]]) if hi > lo else np.zeros(0, np.int64)
+        out["addr"][lo:hi] = np.where(inr[lo:hi], (start + r[lo:hi]).astype(np.uint64), np.uint64(OUT_OF_RANGE))
+        sizes.append(int(slot[lo:hi].sum()))
+    return out, sizes
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("umem_addr", [0x7f0000000000, 0x7f0000000007])
+def test_c_pack_plan_equals_numpy(world, umem_addr):
+    """The packed scatter's layout (xsknf_gpu_shard_pack_plan, the C multi-device
+    path's frames-only distribution) equals its numpy restatement for every
+    descriptor case: odd starts, edge-case lengths, zero lengths, descriptors
+    outside the UMEM; every slot holds its frame, slots never overlap, and the
+    packed bytes are at most the frames' bytes + 31 per frame."""
+    from xsknf_amd import multi
+    for name, b in _desc_cases():
+        ranges, _ = multi.shard_plan(b.descs, world, b.umem.size)
+        bounds = [lo for lo, _ in ranges] + [ranges[-1][1]]
+        got, sizes = multi.pack_plan(b.descs, bounds, umem_addr, b.umem.size)
+        want, wsizes = _pack_plan_py(b.descs, bounds, umem_addr, b.umem.size)
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), name
+        assert sizes == wsizes, name
+        for k, (lo, hi) in enumerate(ranges):
+            a, ln = got["addr"][lo:hi].astype(np.int64), got["len"][lo:hi].astype(np.int64)
+            live = got["addr"][lo:hi] < np.uint64(1 << 47)
+            assert (a[live] + ln[live] <= sizes[k]).all(), name
+            held = live & (ln > 0)                                   # (a zero-length frame has no bytes to hold)
+            ends = a[held] + ln[held]
+            assert (a[held][1:] >= ends[:-1]).all(), name            # in order, no overlap
+            assert sizes[k] <= int(ln[live].sum()) + 31 * int(live.sum()), name

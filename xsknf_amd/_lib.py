@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "xsknf_gpu_hook_destroy",
     "xsknf_gpu_shard_plan",
     "xsknf_gpu_shard_rebase",
+    "xsknf_gpu_shard_pack_plan",
     "xsknf_gpu_multi_create",
     "xsknf_gpu_multi_scatter",
     "xsknf_gpu_multi_scatter_packed",
@@ -214,6 +215,8 @@ def load() -> ctypes.CDLL:
     lib.xsknf_gpu_shard_rebase.restype = ctypes.c_int
     lib.xsknf_gpu_shard_rebase.argtypes = [vp, u64, u64, u64, vp]
     lib.xsknf_gpu_multi_create.restype = ctypes.c_int
+    lib.xsknf_gpu_shard_pack_plan.restype = ctypes.c_int
+    lib.xsknf_gpu_shard_pack_plan.argtypes = [vp, u64, u64, u64, ctypes.c_uint32, vp, vp, vp]
     lib.xsknf_gpu_multi_create.argtypes = [ctypes.POINTER(vp), vp, ctypes.c_int]
     lib.xsknf_gpu_multi_scatter.restype = ctypes.c_int
     lib.xsknf_gpu_multi_scatter.argtypes = [vp, ctypes.c_int, vp, u64, vp, u64, ctypes.POINTER(ctypes.c_double)]

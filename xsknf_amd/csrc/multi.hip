@@ -216,7 +216,8 @@ struct Shard {
   uint64_t lo = 0, hi = 0;       // frames [lo, hi) of the global batch
   uint64_t b0 = 0, b1 = 0;       // its UMEM byte span on the root
   uint64_t bytes = 0;            // sum of the shard's frame lengths
-  uint8_t *umem = nullptr;       // b1 - b0 bytes + 16 spare (the kernels' 16-byte chunk loads)
+  uint8_t *umem = nullptr;       // b1 - b0 bytes + 16 spare (the kernels' 16-byte chunk loads), inside umem_alloc
+  uint8_t *umem_alloc = nullptr; // at the root's address mod kPlace (span scatter): the same placement as there
   uint64_t umem_cap = 0;
   xsknf_gpu_desc *descs = nullptr;
   int32_t *verdicts = nullptr;
@@ -291,15 +292,23 @@ hipError_t stage_root(xsknf_gpu_multi *m, int root, const xsknf_gpu_desc *descs,
 
 // A shard's device buffers for `span` bytes (+ 16 spare: the kernels' 16-byte
 // chunk loads) and `frames` descriptors / verdicts; the spare bytes zeroed.
-hipError_t shard_buffers(Shard &s, uint64_t span, uint64_t frames) {
+// The span starts at address `place` mod kPlace, so that a shard of a UMEM's
+// span keeps the placement its frames had on the root (the channels a frame's
+// sectors fall on follow the address: config 4's 64-B frames at 2 KiB strides).
+constexpr uint64_t kPlace = 4096;
+hipError_t shard_buffers(Shard &s, uint64_t span, uint64_t frames, uint64_t place) {
   hipError_t e = hipSetDevice(s.device);
-  const uint64_t need = span + 16;
+  const uint64_t need = span + 16 + kPlace;
   if (e == hipSuccess && need > s.umem_cap) {
-    if (s.umem) (void)hipFree(s.umem);
-    s.umem = nullptr;
+    if (s.umem_alloc) (void)hipFree(s.umem_alloc);
+    s.umem_alloc = s.umem = nullptr;
     s.umem_cap = 0;
-    e = hipMalloc(&s.umem, need);
+    e = hipMalloc(&s.umem_alloc, need);
     if (e == hipSuccess) s.umem_cap = need;
+  }
+  if (e == hipSuccess) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(s.umem_alloc);
+    s.umem = s.umem_alloc + ((place - a) & (kPlace - 1));
   }
   if (e == hipSuccess && frames > s.frames_cap) {
     if (s.descs) (void)hipFree(s.descs);
@@ -401,6 +410,34 @@ int xsknf_gpu_shard_rebase(const struct xsknf_gpu_desc *descs, uint64_t n, uint6
   return 0;
 }
 
+int xsknf_gpu_shard_pack_plan(const struct xsknf_gpu_desc *descs, uint64_t n, uint64_t umem_addr,
+                              uint64_t umem_size, uint32_t nshards, const uint64_t *bounds,
+                              struct xsknf_gpu_desc *packed, uint64_t *sizes) {
+  if (nshards == 0 || !bounds || !sizes || (n && (!descs || !packed))) return -EINVAL;
+  if (bounds[0] != 0 || bounds[nshards] != n) return -EINVAL;
+  // shard k's frames in global order, each in its own 16-byte aligned slot at
+  // the same address mod 16 as in the UMEM (so the kernels read it exactly as
+  // there); the descriptors each shard receives address its own packed bytes
+  for (uint32_t k = 0; k < nshards; ++k) {
+    if (bounds[k + 1] < bounds[k]) return -EINVAL;
+    uint64_t pos = 0;
+    for (uint64_t f = bounds[k]; f < bounds[k + 1]; ++f) {
+      const xsknf_gpu_desc d = descs[f];
+      packed[f].len = d.len;
+      packed[f].options = d.options;
+      if (!in_umem(d, umem_size)) {
+        packed[f].addr = kOutOfRange;
+        continue;
+      }
+      const uint64_t rs = (umem_addr + umem_offset(d.addr)) & 15;
+      packed[f].addr = pos + rs;
+      pos += d.len ? (rs + d.len + 15) & ~15ull : 0;
+    }
+    sizes[k] = pos;
+  }
+  return 0;
+}
+
 int xsknf_gpu_multi_create(struct xsknf_gpu_multi **out, const int *devices, int ndev) {
   if (!out || ndev < 1 || ndev > 64) return -EINVAL;
   *out = nullptr;
@@ -466,7 +503,7 @@ int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, const uint8_t *
     s.pack_lo = 0;
     s.bytes = 0;
     for (uint64_t f = s.lo; f < s.hi; ++f) s.bytes += descs[f].len;
-    e = shard_buffers(s, s.b1 - s.b0, s.hi - s.lo);
+    e = shard_buffers(s, s.b1 - s.b0, s.hi - s.lo, reinterpret_cast<uintptr_t>(umem) + s.b0);
     if (e != hipSuccess) return hip_fail(e, "multi scatter: shard buffers");
   }
   // every shard at once: the root sends each its span and descriptors, every
@@ -495,30 +532,15 @@ int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const ui
   std::vector<uint64_t> bounds(N + 1);
   int rc = xsknf_gpu_shard_plan(descs, n, umem_size, static_cast<uint32_t>(N), bounds.data(), nullptr);
   if (rc) return rc;
-  // the packed layout: shard k's frames in global order, each in its own
-  // 16-byte aligned slot at the same address mod 16 as in the UMEM; the
-  // descriptors each shard receives address its own packed bytes
   std::vector<xsknf_gpu_desc> packed(n);
   std::vector<uint64_t> pk_lo(N), pk_size(N);
-  const uintptr_t ubase = reinterpret_cast<uintptr_t>(umem);
+  rc = xsknf_gpu_shard_pack_plan(descs, n, reinterpret_cast<uintptr_t>(umem), umem_size, static_cast<uint32_t>(N),
+                                 bounds.data(), packed.data(), pk_size.data());
+  if (rc) return rc;
   uint64_t total = 0;
   for (int k = 0; k < N; ++k) {
-    uint64_t pos = 0;
-    for (uint64_t f = bounds[k]; f < bounds[k + 1]; ++f) {
-      const xsknf_gpu_desc d = descs[f];
-      packed[f].len = d.len;
-      packed[f].options = d.options;
-      if (!in_umem(d, umem_size)) {
-        packed[f].addr = kOutOfRange;
-        continue;
-      }
-      const uint64_t rs = (ubase + umem_offset(d.addr)) & 15;
-      packed[f].addr = pos + rs;
-      pos += d.len ? (rs + d.len + 15) & ~15ull : 0;
-    }
     pk_lo[k] = total;
-    pk_size[k] = pos;
-    total += pos;
+    total += pk_size[k];
   }
   hipError_t e = stage_root(m, root, descs, packed.data(), n);
   if (e == hipSuccess) e = root_buffer(m->root_pack, m->root_pack_cap, total);
@@ -532,7 +554,7 @@ int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const ui
     s.pack_lo = pk_lo[k];
     s.bytes = 0;
     for (uint64_t f = s.lo; f < s.hi; ++f) s.bytes += descs[f].len;
-    e = shard_buffers(s, pk_size[k], s.hi - s.lo);
+    e = shard_buffers(s, pk_size[k], s.hi - s.lo, 0);
     if (e != hipSuccess) return hip_fail(e, "multi packed scatter: shard buffers");
   }
   const double t0 = now_s();
@@ -722,7 +744,7 @@ int xsknf_gpu_multi_destroy(struct xsknf_gpu_multi *m) {
   for (Shard &s : m->sh) {
     if (hipSetDevice(s.device) != hipSuccess) continue;
     if (s.stream) (void)hipStreamSynchronize(s.stream);
-    if (s.umem) (void)hipFree(s.umem);
+    if (s.umem_alloc) (void)hipFree(s.umem_alloc);
     if (s.descs) (void)hipFree(s.descs);
     if (s.verdicts) (void)hipFree(s.verdicts);
     if (s.counters) (void)hipFree(s.counters);

@@ -52,6 +52,21 @@ def shard_rebase(descs, b0: int, umem_size: int) -> np.ndarray:
     return out
 
 
+def pack_plan(descs, bounds, umem_addr: int, umem_size: int):
+    """(packed descriptors, [packed bytes per shard]) of xsknf_gpu_shard_pack_plan
+    for shard bounds [b0 = 0, b1, ..., n], from the C library (no GPU)."""
+    lib = _lib.load()
+    d = _descs_array(descs)
+    n = int(d.shape[0])
+    b = np.ascontiguousarray(np.asarray(bounds, dtype=np.uint64))
+    out = np.zeros_like(d)
+    sizes = np.zeros(b.size - 1, dtype=np.uint64)
+    _lib.check(lib.xsknf_gpu_shard_pack_plan(d.ctypes.data if n else None, n, umem_addr, umem_size, b.size - 1,
+                                             b.ctypes.data, out.ctypes.data if n else None, sizes.ctypes.data),
+               "xsknf_gpu_shard_pack_plan")
+    return out, [int(x) for x in sizes]
+
+
 class MultiDevice:
     """xsknf_gpu_multi over `devices` (HIP device ids, each once)."""
 
