@@ -162,7 +162,7 @@ def test_c_host_multi_device_cases(dev, case):
     _c_host_multi_run(dev, b.umem, b.descs, b.layout, action=action, nif=nif)
 
 
-def _c_host_packed_round_trip(dev, host, hd, action=0, nif=1, iters=1, mean=0):
+def _c_host_packed_round_trip(dev, host, hd, action=0, nif=1, iters=1, mean=0, base_off=0):
     """The global batch out and back through the C host's multi-device calls over
     every visible device: xsknf_gpu_multi_scatter_packed (each shard's frames
     packed into 16-byte slots on the root, then grouped ncclSend / ncclRecv),
@@ -172,7 +172,11 @@ def _c_host_packed_round_trip(dev, host, hd, action=0, nif=1, iters=1, mean=0):
     reference's own pass over the whole batch, byte for byte."""
     from xsknf_amd import ChecksummerOptions, _lib, multi
     ndev = torch.cuda.device_count()
-    umem = torch.from_numpy(host).to(dev)
+    # the root's UMEM `base_off` bytes into its allocation (a base that is not
+    # 16-byte aligned: frames whose first 16-byte chunk starts before it)
+    big = torch.zeros(host.size + base_off + 64, dtype=torch.uint8, device=dev)
+    umem = big[base_off:base_off + host.size]
+    umem.copy_(torch.from_numpy(host))
     n = hd.shape[0]
     v = torch.full((max(n, 1),), 0x7eadbeef, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
@@ -232,7 +236,7 @@ def test_c_host_packed_round_trip_config4(dev):
 
 
 @pytest.mark.parametrize("case", ["unaligned-edges", "jumbo", "out-of-range", "drop-2if", "one-frame", "64B-iter3",
-                                  "ihl-overlap", "empty"])
+                                  "ihl-overlap", "empty", "odd-base-and-end"])
 def test_c_host_packed_round_trip_cases(dev, case):
     """Packed frames at odd addresses (unaligned UMEM, 10 % edge cases), jumbo
     frames, descriptors outside the UMEM, DROP with two interfaces, one frame,
@@ -258,9 +262,20 @@ def test_c_host_packed_round_trip_cases(dev, case):
     elif case == "ihl-overlap":
         b = frames.unaligned_batch(4000, "imix", seed=68)
         frames.inject_edge_cases(b, 0.3, seed=69)
-    else:
+    elif case == "empty":
         b = frames.aligned_batch(1, 570, seed=70)
         b = frames.HostBatch(b.umem, b.descs[:0].copy(), b.layout)
+    else:
+        # packed frames from the UMEM's first byte to its last, the UMEM 7 bytes
+        # into its allocation: the first and last 16-byte chunks reach outside it
+        b = frames.unaligned_batch(3000, "imix", seed=71)
+        a = b.descs["addr"]
+        off = (a & np.uint64((1 << 48) - 1)) + (a >> np.uint64(48))
+        b.descs["addr"] = off - off[0]          # (aligned-mode addresses: plain offsets)
+        end = int((b.descs["addr"] + b.descs["len"]).max())
+        umem = b.umem[int(off[0]):int(off[0]) + end].copy()
+        _c_host_packed_round_trip(dev, umem, b.descs, base_off=7)
+        return
     _c_host_packed_round_trip(dev, b.umem, b.descs, action=action, nif=nif, iters=iters)
 
 
