@@ -45,7 +45,14 @@ HOOKBENCH := tools/build/hook_bench
 CTXLAT := tools/build/ctx_latency
 BARPROBE := tools/build/bar_probe
 DEVPROBE := tools/build/dev_probe
-tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH) $(CTXLAT) $(BARPROBE) $(DEVPROBE)
+MULTIC4 := tools/build/multi_config4
+tools: $(VETH) $(PROBE) $(PROBELIB) $(HOOKBENCH) $(CTXLAT) $(BARPROBE) $(DEVPROBE) $(MULTIC4)
+# config 4 through the multi-device calls from a C host (checked against the CPU oracle)
+$(MULTIC4): tools/multi_config4.c $(LIB) oracle
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -g -std=gnu11 -Wall -Wextra -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+		-L$(LIBDIR) -lxsknf_gpu -Loracle/build -lcsum_oracle -L/opt/rocm/lib -lamdhip64 \
+		-Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -Wl,-rpath,/opt/rocm/lib
 # one NF-shaped process start (device count, a context), for tools/nf_start_probe.py
 $(DEVPROBE): tools/dev_probe.c $(LIB)
 	@mkdir -p $(dir $@)

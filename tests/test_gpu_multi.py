@@ -279,6 +279,30 @@ def test_c_host_packed_round_trip_cases(dev, case):
     _c_host_packed_round_trip(dev, b.umem, b.descs, action=action, nif=nif, iters=iters)
 
 
+def _run_tool(cmd, timeout):
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    return p.returncode, p.stdout, p.stderr
+
+
+@pytest.mark.parametrize("frames_n", [1, 65537, 1 << 20])
+def test_c_host_tool_config4_shape(dev, clean_ctx, frames_n):
+    """tools/multi_config4.c: a C host drives the multi-device calls itself
+    (xsknf_gpu_multi_create / _scatter / _process / _counters, then
+    _scatter_packed / _return), over every device of the box, on an IMIX batch in
+    config 4's layout; its own check against the CPU oracle -- the all-reduced
+    counters, the root's UMEM and verdicts after the return -- must hold.  (Run
+    from the forkserver, never from this GPU-initialised process.)"""
+    tool = os.path.join(ROOT, "tools", "build", "multi_config4")
+    if not os.path.exists(tool):
+        pytest.fail(f"{tool} is not built (make tools)")
+    with clean_ctx.Pool(1) as pool:
+        rc, out, err = pool.apply(_run_tool, ([tool, str(frames_n)], 300))
+    assert rc == 0, (out, err[-2000:])
+    r = json.loads(out.strip().splitlines()[-1])
+    assert r["frames"] == frames_n and r["counters_match"] and r["root_umem_match"] and r["verdicts_match"]
+    assert r["frame_bytes"] <= r["packed_bytes"] <= r["frame_bytes"] + 31 * frames_n
+
+
 def _scatter_rank(rank, world, port, outdir):
     import torch
     import torch.distributed as dist
