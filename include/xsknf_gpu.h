@@ -408,7 +408,10 @@ XSKNF_GPU_API int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int 
  * order), and a kernel on the root writes each record's check into `umem` (the
  * root UMEM the scatter read, at the frame the caller's descriptor names) and
  * turns it into the forward verdict.  `umem` and `verdicts` then hold what one
- * device's xsknf_gpu_checksum_batch over the whole batch leaves.  ms (may be
+ * device's xsknf_gpu_checksum_batch over the whole batch leaves.  -EBUSY when
+ * xsknf_gpu_multi_process has checksummed the shards in place since the
+ * scatter (a second pass is not the first: a frame whose UDP header overlaps
+ * its IP addresses sums the check the first wrote); scatter again.  ms (may be
  * NULL, ndev entries): each device's summing pass, HIP events; seconds (may be
  * NULL): the whole return. */
 XSKNF_GPU_API int xsknf_gpu_multi_return(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex,

@@ -162,7 +162,7 @@ def test_c_host_multi_device_cases(dev, case):
     _c_host_multi_run(dev, b.umem, b.descs, b.layout, action=action, nif=nif)
 
 
-def _c_host_packed_round_trip(dev, host, hd, action=0, nif=1, iters=1, mean=0, base_off=0):
+def _c_host_packed_round_trip(dev, host, hd, action=0, nif=1, iters=1, mean=0, base_off=0, process_first=False):
     """The global batch out and back through the C host's multi-device calls over
     every visible device: xsknf_gpu_multi_scatter_packed (each shard's frames
     packed into 16-byte slots on the root, then grouped ncclSend / ncclRecv),
@@ -205,6 +205,14 @@ def _c_host_packed_round_trip(dev, host, hd, action=0, nif=1, iters=1, mean=0, b
                 p, L = int(sd["addr"][f - lo]), int(ln[f])
                 assert p % 16 == (umem.data_ptr() + int(off[f])) % 16
                 assert np.array_equal(su[p:p + L], host[off[f]:off[f] + L]), f"frame {f} packed bytes"
+        if process_first:
+            # the shards checksummed in place first: a return now would describe a
+            # second pass, so it is refused (-EBUSY) until the batch is scattered again
+            m.process(ChecksummerOptions(action=action, csum_iterations=iters), num_interfaces=nif,
+                      frame_len_max=int(hd["len"].max()) if n else 0)
+            with pytest.raises(_lib.XsknfGpuError, match="rc=-16"):
+                m.return_results(umem.data_ptr(), v.data_ptr())
+            m.scatter_packed(0, umem.data_ptr(), umem.numel(), hd)
         ms, secs2 = m.return_results(umem.data_ptr(), v.data_ptr(), ChecksummerOptions(action=action,
                                                                                          csum_iterations=iters),
                                      num_interfaces=nif, frame_len_max=int(hd["len"].max()) if n else 0,
@@ -236,7 +244,7 @@ def test_c_host_packed_round_trip_config4(dev):
 
 
 @pytest.mark.parametrize("case", ["unaligned-edges", "jumbo", "out-of-range", "drop-2if", "one-frame", "64B-iter3",
-                                  "ihl-overlap", "empty", "odd-base-and-end"])
+                                  "ihl-overlap", "empty", "odd-base-and-end", "processed-first"])
 def test_c_host_packed_round_trip_cases(dev, case):
     """Packed frames at odd addresses (unaligned UMEM, 10 % edge cases), jumbo
     frames, descriptors outside the UMEM, DROP with two interfaces, one frame,
@@ -262,6 +270,11 @@ def test_c_host_packed_round_trip_cases(dev, case):
     elif case == "ihl-overlap":
         b = frames.unaligned_batch(4000, "imix", seed=68)
         frames.inject_edge_cases(b, 0.3, seed=69)
+    elif case == "processed-first":
+        b = frames.aligned_batch(20000, "imix", seed=72)
+        frames.inject_edge_cases(b, 0.05, seed=73)
+        _c_host_packed_round_trip(dev, b.umem, b.descs, process_first=True)
+        return
     elif case == "empty":
         b = frames.aligned_batch(1, 570, seed=70)
         b = frames.HostBatch(b.umem, b.descs[:0].copy(), b.layout)

@@ -239,6 +239,7 @@ struct xsknf_gpu_multi {
   int root = -1;                          // index of the root of the last scatter
   uint64_t n = 0;                         // frames of the last scatter
   bool packed = false;                    // the last scatter moved packed frames
+  bool processed = false;                 // _process wrote checks into the shards since the last scatter
   // on the root device (root_descs_dev): the last scatter's descriptors as the
   // caller gave them (for the results' return) and the packed staging buffer
   xsknf_gpu_desc *root_orig = nullptr;
@@ -521,6 +522,7 @@ int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, const uint8_t *
   if (seconds) *seconds = now_s() - t0;
   m->root = root;
   m->n = n;
+  m->processed = false;
   m->packed = false;
   return 0;
 }
@@ -584,6 +586,7 @@ int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const ui
   if (seconds) *seconds = now_s() - t0;
   m->root = root;
   m->n = n;
+  m->processed = false;
   m->packed = true;
   return 0;
 }
@@ -604,6 +607,7 @@ int xsknf_gpu_multi_process(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex,
     if (rc) return rc;
     e = hipEventRecord(s.e1, s.stream);
     if (e != hipSuccess) return hip_fail(e, "multi process: end");
+    m->processed = true;
   }
   for (int k = 0; k < m->ndev; ++k) {
     Shard &s = m->sh[k];
@@ -661,6 +665,14 @@ int xsknf_gpu_multi_return(struct xsknf_gpu_multi *m, uint32_t ingress_ifindex, 
                            uint32_t frame_len_max, uint32_t frame_len_mean, uint8_t *umem, int32_t *verdicts, float *ms,
                            double *seconds) {
   if (!m || !opts || m->root < 0 || (m->n && (!umem || !verdicts))) return -EINVAL;
+  // the records describe a pass over the frames as the scatter sent them: once
+  // _process has rewritten checks in the shards, a second pass is not the same
+  // (a frame whose UDP header overlaps its IP addresses, ihl 2 or 3, sums the
+  // check it just wrote), so the caller scatters again
+  if (m->processed) {
+    xsknf_gpu::set_error_text("xsknf_gpu_multi_return: the shards were checksummed in place since the scatter");
+    return -EBUSY;
+  }
   xsknf_gpu_launch_cfg cfg;
   int rc = xsknf_gpu_launch_cfg_for_lens(frame_len_max, frame_len_mean, &cfg);
   if (rc) return rc;
