@@ -1057,6 +1057,28 @@ def test_grid_sizing_on_a_smaller_device(length, n, window):
     assert r["pool_guard_trips"] == 0, r
 
 
+@pytest.mark.skipif(not AB_BUILD, reason="A/B build only (XSKNF_AB_NO_GRID_BOUND)")
+def test_pool_guard_trips_without_the_grid_bound():
+    """The pool guard works: in the A/B build with launch_split's grid bound left
+    out (XSKNF_AB_NO_GRID_BOUND) and the grids sized for 4 CUs, a 30720-frame
+    jumbo batch gives each pool block 120 tiles, more units than its waves'
+    20-unit lists hold; the waves stop claiming, units go unclaimed, their
+    frames stay unsummed, and xsknf_gpu_pool_guard_trips counts it (with the
+    bound, the same batch is bit-exact and the count 0:
+    test_grid_sizing_on_a_smaller_device)."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, XSKNF_GPU_CU_LIMIT="4", XSKNF_AB_NO_GRID_BOUND="1")
+    out = subprocess.run([sys.executable, os.path.join(root, "tests", "cu_limit_child.py"), "--frames", "30720",
+                          "--length", "9000", "--layout", "unaligned"],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["window_chunks"] == 52 and r["pool_guard_trips"] > 0, r
+    assert r["bad_bytes"] > 0 or r["bad_verdicts"] > 0, r
+
+
 @pytest.mark.parametrize("shape", [(16, 2, 2, 0, 18, 1, 56), (16, 3, 2, 0, 18, 1, 52), (16, 3, 2, 0, 0, 1, 52),
                                    pytest.param((1, 5, 2, 0, 1, 0, 32),
                                                 marks=pytest.mark.skipif(not AB_BUILD, reason="A/B build only")),

@@ -2261,7 +2261,7 @@ int launch_split(const KernelArgs &a, hipStream_t stream, int blocks_per_cu) {
     // (Kept from the investigation of the GPU suites' illegal-address faults,
     // whose cause was HIP's locked-pageable-memory copy in the test process,
     // not these kernels -- DESIGN 3; tested by test_no_wave_passes_its_patch_list.)
-    if (a.tail_scatter) {
+    if (a.tail_scatter && !ab_no_grid_bound()) {   // (A/B builds can leave it out to exercise the guard)
       const uint32_t tiles = (a.n + kWave - 1) / kWave;
       // (a pool block of bt >= k * SW tiles has bt + (parts - 1) * k * SW units,
       // k * SW of them split, and its waves' lists hold SW * PT: so at most
