@@ -1192,8 +1192,9 @@ constexpr uint32_t pool_block_tiles_max(int w, int sw, int pt) {
 // Pool guard: a pooled wave whose patch list is full claims no more units, so
 // a grid too small for the batch would leave units unclaimed (their frames
 // unsummed).  launch_split's bound makes that unreachable; should it ever be
-// reached, the block's patch queue waits for a unit that never comes, and each
-// wave that gives up counts here (xsknf_gpu_pool_guard_trips reads it).
+// reached, each block with more units than its waves' lists hold counts here
+// at its start, and each wave that waits in vain for a unit's mark in the
+// patch queue counts too (xsknf_gpu_pool_guard_trips reads it).
 __device__ unsigned int g_pool_guard_trips;
 
 // The pooled jumbo shape (W = 4, 16 x 3 items, one 8-wave block per CU) keeps
@@ -1418,6 +1419,11 @@ void checksum_kernel_split(const KernelArgs args) {
   uint32_t block_units = 0;
   if constexpr (kShared) {
     block_units = units;
+    // more units than the waves' lists hold: the waves stop claiming once their
+    // lists are full, so units are left unclaimed (never, by launch_split's bound;
+    // the same count the marks below would wait for in vain)
+    if (threadIdx.x == 0 && shared_on && units > kPQ)
+      __hip_atomic_fetch_add(&g_pool_guard_trips, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) pq_tail = pq_head = 0;
     for (uint32_t i = threadIdx.x; i < kPQ; i += SW * kWave) pq[i] = 0;
     __syncthreads();
