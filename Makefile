@@ -4,7 +4,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-inline-asm -fvisibility=hidden --offload-arch=$(ARCH) -Iinclude
 LIBDIR := xsknf_amd/lib
 LIB := $(LIBDIR)/libxsknf_gpu.so
-SRCS := xsknf_amd/csrc/checksummer.hip xsknf_amd/csrc/host_path.hip xsknf_amd/csrc/multi.hip
+SRCS := xsknf_amd/csrc/checksummer.hip xsknf_amd/csrc/host_path.hip xsknf_amd/csrc/multi.hip xsknf_amd/csrc/shard_plan.cpp
 # RCCL for the multi-device calls (xsknf_gpu_multi_*)
 GPULIBS := -L/opt/rocm/lib -lrccl
 
