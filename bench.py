@@ -25,6 +25,12 @@ at N = 1, exactly config 4's 8-way split at N = 8); the NIC-checksummed variants
 (`*-nic`); and `64-13M`, config 2's frames as one 13M-frame batch (one
 lane-kernel launch instead of 13: what a 64 B step costs without its launch's
 ramp and drain).
+
+At world 1 the line ends with `c_host_multi`: config 4 through the C host's
+multi-device calls over every visible device of this one process (span
+scatter, in-place steps, all-reduced counters; then the frames-only packed
+scatter and the results' return, checked byte for byte against one device's
+pass), run last behind a watchdog so that it cannot cost the line.
 """
 from __future__ import annotations
 
