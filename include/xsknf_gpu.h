@@ -352,8 +352,8 @@ struct xsknf_gpu_shard_info {
 	int32_t device;          /* HIP device of the shard */
 	uint32_t flags;          /* XSKNF_GPU_SHARD_PACKED */
 	uint64_t frame_lo, frame_hi;   /* frames [lo, hi) of the global batch */
-	uint64_t span_lo, span_hi;     /* its bytes [lo, hi) of the root's UMEM (packed: of the root's
-	                                  packed buffer, the shard's own bytes starting at 0) */
+	uint64_t span_lo, span_hi;     /* its bytes [lo, hi) of the root's UMEM (packed: 0 and the
+	                                  shard's packed bytes) */
 	uint64_t frame_bytes;          /* sum of its frame lengths */
 	uint8_t *umem;                 /* device buffers of the shard on its device */
 	struct xsknf_gpu_desc *descs;
@@ -396,8 +396,10 @@ XSKNF_GPU_API int xsknf_gpu_multi_counters(struct xsknf_gpu_multi *m, uint64_t *
  * buffer (a frame keeps its address mod 16; the bytes that share its first and
  * last 16-byte chunk travel with it), and each shard receives its packed bytes
  * plus descriptors that address them (aligned-mode addresses; descriptors
- * outside the UMEM keep their length and get an address past any span).  A
- * UMEM of 2 KiB chunks holding IMIX frames moves ~1/5 of its span bytes.
+ * outside the UMEM keep their length and get an address past any span).  The
+ * root's own shard is packed straight into its shard buffer (its descriptors
+ * still go as a send to itself).  A UMEM of 2 KiB chunks holding IMIX frames
+ * moves ~1/5 of its span bytes.
  * seconds (may be NULL): the packing and the moves. */
 XSKNF_GPU_API int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const uint8_t *umem,
 		uint64_t umem_size, const struct xsknf_gpu_desc *descs, uint64_t n, double *seconds);

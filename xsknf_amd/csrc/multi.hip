@@ -209,7 +209,7 @@ struct Shard {
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   uint64_t lo = 0, hi = 0;       // frames [lo, hi) of the global batch
-  uint64_t b0 = 0, b1 = 0;       // its UMEM byte span on the root
+  uint64_t b0 = 0, b1 = 0;       // its UMEM byte span on the root (packed: 0 and its packed bytes)
   uint64_t bytes = 0;            // sum of the shard's frame lengths
   uint8_t *umem = nullptr;       // b1 - b0 bytes + 16 spare (the kernels' 16-byte chunk loads), inside umem_alloc
   uint8_t *umem_alloc = nullptr; // at the root's address mod kPlace (span scatter): the same placement as there
@@ -218,7 +218,6 @@ struct Shard {
   int32_t *verdicts = nullptr;
   uint64_t frames_cap = 0;
   unsigned long long *counters = nullptr;   // device: XSKNF_GPU_MULTI_COUNTERS
-  uint64_t pack_lo = 0;          // packed scatter: the shard's bytes [pack_lo, pack_lo + b1 - b0) of the root's packed buffer
 };
 
 }  // namespace
@@ -416,7 +415,6 @@ int xsknf_gpu_multi_scatter(struct xsknf_gpu_multi *m, int root, const uint8_t *
     s.hi = bounds[k + 1];
     s.b0 = spans[2 * k];
     s.b1 = spans[2 * k + 1];
-    s.pack_lo = 0;
     s.bytes = 0;
     for (uint64_t f = s.lo; f < s.hi; ++f) s.bytes += descs[f].len;
     e = shard_buffers(s, s.b1 - s.b0, s.hi - s.lo, reinterpret_cast<uintptr_t>(umem) + s.b0);
@@ -454,10 +452,12 @@ int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const ui
   rc = xsknf_gpu_shard_pack_plan(descs, n, reinterpret_cast<uintptr_t>(umem), umem_size, static_cast<uint32_t>(N),
                                  bounds.data(), packed.data(), pk_size.data());
   if (rc) return rc;
+  // the root's own shard is packed straight into its shard buffer; the staging
+  // buffer holds the others' (at N = 1 nothing is staged, nothing copied)
   uint64_t total = 0;
   for (int k = 0; k < N; ++k) {
-    pk_lo[k] = total;
-    total += pk_size[k];
+    pk_lo[k] = k == root ? 0 : total;
+    total += k == root ? 0 : pk_size[k];
   }
   hipError_t e = stage_root(m, root, descs, packed.data(), n);
   if (e == hipSuccess) e = root_buffer(m->root_pack, m->root_pack_cap, total);
@@ -468,7 +468,6 @@ int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const ui
     s.hi = bounds[k + 1];
     s.b0 = 0;
     s.b1 = pk_size[k];
-    s.pack_lo = pk_lo[k];
     s.bytes = 0;
     for (uint64_t f = s.lo; f < s.hi; ++f) s.bytes += descs[f].len;
     e = shard_buffers(s, pk_size[k], s.hi - s.lo, 0);
@@ -476,7 +475,7 @@ int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const ui
   }
   const double t0 = now_s();
   // gather every shard's frames on the root, on the root's stream (its sends
-  // follow on the same stream)
+  // follow on the same stream): the root's own into its shard buffer
   Shard &rs = m->sh[root];
   e = hipSetDevice(rs.device);
   for (int k = 0; k < N && e == hipSuccess; ++k) {
@@ -485,14 +484,15 @@ int xsknf_gpu_multi_scatter_packed(struct xsknf_gpu_multi *m, int root, const ui
     const uint64_t want = (frames + 255) / 256;
     const unsigned grid = static_cast<unsigned>(want < 4096 ? want : 4096);
     hipLaunchKernelGGL(pack_frames, dim3(grid), dim3(256), 0, rs.stream, umem, umem_size, m->root_orig + bounds[k],
-                       m->root_descs + bounds[k], frames, m->root_pack + pk_lo[k]);
+                       m->root_descs + bounds[k], frames, k == root ? rs.umem : m->root_pack + pk_lo[k]);
     e = hipGetLastError();
   }
   if (e != hipSuccess) return hip_fail(e, "multi packed scatter: pack_frames");
   std::vector<Move> moves;
   for (int k = 0; k < N; ++k) {
     Shard &s = m->sh[k];
-    moves.push_back({m->root_pack + pk_lo[k], s.umem, pk_size[k], root, k});
+    if (k != root) moves.push_back({m->root_pack + pk_lo[k], s.umem, pk_size[k], root, k});
+    // (the root's descriptors too, as a send to itself: the same path at N = 1)
     moves.push_back({reinterpret_cast<const uint8_t *>(m->root_descs + s.lo), reinterpret_cast<uint8_t *>(s.descs),
                      sizeof(xsknf_gpu_desc) * (s.hi - s.lo), root, k});
   }
@@ -643,8 +643,8 @@ int xsknf_gpu_multi_shard_info(const struct xsknf_gpu_multi *m, int k, struct xs
   info->flags = m->packed ? XSKNF_GPU_SHARD_PACKED : 0;
   info->frame_lo = s.lo;
   info->frame_hi = s.hi;
-  info->span_lo = m->packed ? s.pack_lo : s.b0;
-  info->span_hi = m->packed ? s.pack_lo + s.b1 : s.b1;
+  info->span_lo = s.b0;   // (packed: 0 .. the shard's packed bytes)
+  info->span_hi = s.b1;
   info->frame_bytes = s.bytes;
   info->umem = s.umem;
   info->descs = s.descs;
