@@ -603,8 +603,9 @@ def c_host_multi_leg(args, dev, reps=10):
               "round_trip_ms": round((t_pk + t_ret) * 1e3, 3),
               "step_us_on_packed_shards": round(sorted(max(st) for st in psteps)[len(psteps) // 2] * 1e3, 2),
               "match": round_trip_match,
-              "what": "frames packed into 16-byte slots on device 0 and sent (grouped ncclSend / ncclRecv); each "
-                      "device's records-only pass; 4 B per frame back; the checks applied to device 0's UMEM -- "
+              "what": "frames packed into 16-byte slots on device 0 (its own shard straight into its shard buffer, "
+                      "the others' sent by grouped ncclSend / ncclRecv; scatter_bytes: every shard's packed bytes); "
+                      "each device's records-only pass; 4 B per frame back; the checks applied to device 0's UMEM -- "
                       "match: device 0's UMEM and verdicts equal one device's pass over the whole batch, every "
                       "byte (medians of 3)"}
     del umem, dt, v, pristine, vret
